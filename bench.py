@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Benchmark: delivered packets/s of the batched Chandy-Lamport engine (BASELINE.json).
+
+A step = one pass of the hot path over one batch: every instance of the batch runs the
+whole event program (BASELINE config 2: 10nodes.top + 10nodes.events, 65,536 replicas
+per GPU, each with its own Go delay stream) from the initial topology to the end of the
+drain (test_common.go:79-140).  Inputs (topology, event program, delay schedule) are
+resident in HBM before timing; the timed region is K launches of the exec kernel.
+
+Multi-GPU: one process per GPU, each owning a disjoint instance range (seeds
+base + rank * I + i); instances are independent so there is no data-path collective
+("scaling": "weak").  RCCL all-reduces the batch checksums once, after timing.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §6 for the byte model behind "roofline".
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "chandy-lamport-distributed-snapshot-algorithm_amd"
+TEST_DATA = os.path.join(ROOT, "tests", "golden", "test_data")
+
+CONFIGS = {
+    # BASELINE.json configs[1]: the headline single-GPU workload
+    "c2": ("10nodes.top", "10nodes.events", 65536,
+           "10nodes.top + 10nodes.events, 65,536 replicas per GPU, Go delay streams"),
+    # BASELINE.json configs[2]: 2^20 instances over 8 GPUs = 131,072 per GPU
+    "c3": ("8nodes.top", "8nodes-concurrent-snapshots.events", 131072,
+           "8nodes.top + 8nodes-concurrent-snapshots.events, 131,072 instances per GPU"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def b_alg(c, n_nodes):
+    """8 push + 8 peek + 8 pop + 4 recorded + 1 draw + 4 N completed."""
+    pops = c["pop_tok"] + c["pop_mk"]
+    return 8 * c["push"] + 8 * c["peek"] + 8 * pops + 4 * c["recorded"] + 1 * c["push"] \
+        + 4 * n_nodes * c["completed"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--instances", type=int, default=0, help="instances per GPU (default: config)")
+    ap.add_argument("--fifo-slots", type=int, default=8)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    top, events, per_gpu, desc = CONFIGS[args.config]
+    if args.instances:
+        per_gpu = args.instances
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    cl = importlib.import_module(PKG)
+    seed_base = cl.REFERENCE_SEED + rank * per_gpu
+    sim = cl.ChandyLamportSim(per_gpu, device=local_rank, seed_base=seed_base,
+                              fifo_lds_slots=args.fifo_slots)
+    sim.read_topology_file(os.path.join(TEST_DATA, top))
+    sim.read_events_file(os.path.join(TEST_DATA, events))
+    sim.flush()                      # uploads topology/program/delays, first full run
+    counters = sim.counters(only_ok=False)
+    counters_ok = sim.counters(only_ok=True)
+    n_nodes = sim.num_nodes
+
+    for _ in range(args.warmup):
+        sim.rerun()
+    sim.synchronize()
+    sim.kernel_time()                # reset the per-launch HIP-event accumulator
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sim.rerun()
+    sim.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    k_total_ms, k_launches = sim.kernel_time()   # HIP events around each timed launch
+
+    sums = sim.checksums()
+    t_local = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    s_local = torch.tensor(sums.tolist() + [counters_ok["pop_tok"] + counters_ok["pop_mk"]],
+                           dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
+        dist.all_reduce(s_local, op=dist.ReduceOp.SUM)
+    t_max = float(t_local.item())
+    tot = dict(zip(cl.SUM_NAMES, s_local.tolist()[:len(cl.SUM_NAMES)]))
+    delivered_ok = s_local.tolist()[-1]          # packets of OK instances, all ranks
+
+    per_step = t_max / args.steps
+    value = delivered_ok / per_step
+    avg_kernel_ms = k_total_ms / max(k_launches, 1)
+    alg = b_alg(counters, n_nodes)                  # bytes per launch (this rank)
+    achieved = alg / (avg_kernel_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(top, events, per_gpu, args.cpu_baseline_seconds)
+
+    traffic = None
+    tr_path = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tr_path):
+        with open(tr_path) as f:
+            tr = json.load(f)
+        if tr.get("instances") == per_gpu and tr.get("fifo_slots") == args.fifo_slots:
+            traffic = tr.get("hbm_bytes_per_launch")
+
+    if rank == 0:
+        line = {
+            "metric": "delivered packets/sec (whole node)",
+            "value": value,
+            "unit": "packets/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": per_step * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic: reference test_data scenario, per-instance Go math/rand delay streams",
+            "config": {"workload": desc, "instances_per_gpu": per_gpu,
+                       "instances_total": per_gpu * world, "parallelism": f"instances sharded over {world} GPU(s)",
+                       "fifo_lds_slots": args.fifo_slots},
+            "packets_per_step": delivered_ok,
+            "status": {"ok": tot["ok"], "fatal": tot["fatal"], "other": tot["other"]},
+            "checks": {"cut_residual": tot["cut_residual"], "final_residual": tot["final_residual"],
+                       "snapshot_hash": tot["snapshot_hash"], "completed": tot["completed"]},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "kernel": "cl_exec_kernel",
+                         "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(top, events, n_total, budget_s):
+    """The CPU oracle (C restatement, one simulation per thread) on a bounded sample of
+    the same workload: the first S instances with the same seeds."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    t_text = open(os.path.join(TEST_DATA, top)).read()
+    e_text = open(os.path.join(TEST_DATA, events)).read()
+    probe = 2000
+    secs, st, _, cnt, _ = O.run_batch(t_text, e_text, probe, threads=threads)
+    rate = probe / max(secs, 1e-6)
+    sample = int(min(n_total, max(probe, rate * budget_s)))
+    secs, st, _, cnt, _ = O.run_batch(t_text, e_text, sample, threads=threads)
+    ok = st == 0
+    pkts = int((cnt[ok, 2] + cnt[ok, 3]).sum())
+    return {"value": pkts / secs, "unit": "packets/s", "cores": threads, "kind": "port",
+            "sample": f"first {sample} of {n_total} instances (same seeds), {secs:.1f} s, "
+                      f"CPU restatement in C (oracle/cl_oracle.c), not the Go reference (no Go toolchain)"}
+
+
+if __name__ == "__main__":
+    main()

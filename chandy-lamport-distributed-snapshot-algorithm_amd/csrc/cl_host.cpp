@@ -1,0 +1,1060 @@
+// cl_host.cpp -- host runtime behind include/clsnap.h.
+//
+// The host side mirrors the reference's Simulator API (sim.go, node.go) and its
+// drivers (test_common.go) over a batch of instances:
+//   * topology: AddNode/AddLink collected, then frozen into rank order (getSortedKeys,
+//     common.go:135-146) as out-CSR (channels by (src rank, dest rank)) and in-CSR;
+//   * events: SendTokens / StartSnapshot / Tick / drain become an op program that the
+//     gfx950 kernel executes for every instance (cl_kernels.hip);
+//   * delays: the reference's rand.Intn(5) (sim.go:101) is replayed from a per-instance
+//     schedule, by default Go's own math/rand stream for seed_base + i, restated here;
+//   * results: snapshots are packed back into the reference's {tokenMap, messages}
+//     shape (sim.go:134-173) per instance.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/clsnap.h"
+#include "cl_engine.h"
+
+using namespace clsnap;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_err(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+// ---------------------------------------------------------------------------
+// Go math/rand (Go 1.22, go.mod:3): rngSource seeded as in rng.go, Intn -> Int31n.
+// rngCooked is regenerated offline by oracle/gen_go_rng_cooked.py (KAT-pinned).
+// ---------------------------------------------------------------------------
+const int64_t kRngCooked[607] = {
+#include "go_rng_cooked.inc"
+};
+
+struct GoRand {
+  int tap = 0, feed = 334;
+  uint64_t vec[607];
+
+  static int32_t seedrand(int32_t x) {
+    const int32_t hi = x / 44488, lo = x % 44488;
+    x = 48271 * lo - 3399 * hi;
+    if (x < 0) x += 2147483647;
+    return x;
+  }
+  explicit GoRand(int64_t seed) {
+    seed %= 2147483647LL;
+    if (seed < 0) seed += 2147483647LL;
+    if (seed == 0) seed = 89482311;
+    int32_t x = (int32_t)seed;
+    for (int i = -20; i < 607; ++i) {
+      x = seedrand(x);
+      if (i >= 0) {
+        uint64_t u = (uint64_t)(int64_t)x << 40;
+        x = seedrand(x);
+        u ^= (uint64_t)(int64_t)x << 20;
+        x = seedrand(x);
+        u ^= (uint64_t)(int64_t)x;
+        vec[i] = u ^ (uint64_t)kRngCooked[i];
+      }
+    }
+  }
+  uint64_t uint64() {
+    if (--tap < 0) tap += 607;
+    if (--feed < 0) feed += 607;
+    vec[feed] += vec[tap];
+    return vec[feed];
+  }
+  int64_t int63() { return (int64_t)(uint64() & 0x7fffffffffffffffULL); }
+  int32_t int31() { return (int32_t)(int63() >> 32); }
+  int32_t int31n(int32_t n) {
+    if ((n & (n - 1)) == 0) return int31() & (n - 1);
+    const int32_t max = (int32_t)((1LL << 31) - 1 - (int64_t)((1ULL << 31) % (uint32_t)n));
+    int32_t v = int31();
+    while (v > max) v = int31();
+    return v % n;
+  }
+};
+
+int host_threads() {
+  unsigned n = std::thread::hardware_concurrency();
+  if (n == 0) n = 1;
+  return (int)std::min(n, 16u);  // the GPU box grants 16 host cores per GPU
+}
+
+void go_schedule(int64_t seed_base, int64_t n, int64_t draws, uint8_t* out) {
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), (n + 255) / 256));
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    th.emplace_back([=] {
+      for (int64_t i = n * t / T; i < n * (t + 1) / T; ++i) {
+        GoRand r(seed_base + i);
+        uint8_t* o = out + i * draws;
+        for (int64_t k = 0; k < draws; ++k) o[k] = (uint8_t)r.int31n(5);  // rand.Intn(maxDelay)
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
+// ---------------------------------------------------------------------------
+// Go-style text helpers (strings.Fields, strconv.Atoi, FieldsFunc(s, '\n'))
+// ---------------------------------------------------------------------------
+bool go_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
+
+std::vector<std::string> go_fields(const std::string& s) {
+  std::vector<std::string> f;
+  size_t i = 0;
+  while (i < s.size()) {
+    while (i < s.size() && go_space(s[i])) ++i;
+    if (i >= s.size()) break;
+    size_t j = i;
+    while (j < s.size() && !go_space(s[j])) ++j;
+    f.emplace_back(s.substr(i, j - i));
+    i = j;
+  }
+  return f;
+}
+
+bool go_atoi(const std::string& s, int64_t* out) {
+  size_t i = 0;
+  bool neg = false;
+  if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
+  if (i >= s.size()) return false;
+  int64_t v = 0;
+  for (; i < s.size(); ++i) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    if (v > (INT64_MAX - (s[i] - '0')) / 10) return false;
+    v = v * 10 + (s[i] - '0');
+  }
+  *out = neg ? -v : v;
+  return true;
+}
+
+std::vector<std::string> go_lines(const std::string& s) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i <= s.size()) {
+    size_t j = s.find('\n', i);
+    if (j == std::string::npos) j = s.size();
+    if (j > i) out.emplace_back(s.substr(i, j - i));
+    i = j + 1;
+  }
+  return out;
+}
+
+bool read_file(const char* path, std::string* out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  std::ostringstream ss;
+  ss << f.rdbuf();
+  *out = ss.str();
+  return true;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) return set_err(CL_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int ensure(size_t count) {
+    if (count <= n && p) return CL_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (count == 0) count = 1;
+    HIP_TRY(hipMalloc((void**)&p, count * sizeof(T)));
+    n = count;
+    return CL_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// cl_sim
+// ---------------------------------------------------------------------------
+struct cl_sim {
+  int64_t n_inst = 0;
+  int64_t stride = 0;  // n_inst rounded up to the wave size
+  int device = 0;
+
+  // topology (insertion order until frozen)
+  std::vector<std::string> ids;
+  std::vector<int64_t> init_tokens;
+  std::unordered_map<std::string, int> id_index;
+  std::vector<std::pair<int, int>> links;  // unique (src, dst) in insertion indices
+  bool frozen = false;
+  std::vector<int> rank_of;    // insertion index -> rank
+  std::vector<int> by_rank;    // rank -> insertion index
+  std::vector<int32_t> out_off, ch_dst, ch_src, in_off, in_ch, init_tok;
+  int64_t total_tokens = 0;
+
+  // event program
+  std::vector<Op> ops;
+  int32_t executed = 0;
+  int32_t n_sids = 0;
+  int64_t sends = 0;
+  int64_t time_bound = 0;
+  std::vector<std::vector<int32_t>> hist;  // token history per channel (push order)
+  std::vector<int32_t> depth_bound;        // packets ever pushed per channel
+
+  // limits
+  int32_t cap_log2 = 3;
+  int64_t max_drain = 10000;
+
+  // delays
+  bool go_seeds = true;
+  int64_t seed_base = 8053172852482175524LL;  // snapshot_test.go:9,20 (seed + 1)
+  std::vector<uint8_t> user_sched;
+  int64_t user_draws = 0;
+  int64_t dev_draws = -1;  // row length of the schedule resident on the device
+
+  // device
+  bool dev_ready = false;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;  // per-launch timing events
+  size_t ev_used = 0;
+  double ev_folded_ms = 0;   // time of launches whose events were recycled
+  int64_t ev_folded_n = 0;
+
+  // Fold finished launch timings into the accumulator so the event pool stays bounded.
+  int fold_events() {
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (size_t i = 0; i < ev_used; ++i) {
+      float f = 0.f;
+      HIP_TRY(hipEventElapsedTime(&f, ev_pool[i].first, ev_pool[i].second));
+      ev_folded_ms += f;
+    }
+    ev_folded_n += (int64_t)ev_used;
+    if (ev_used) std::swap(ev_pool[0], ev_pool[ev_used - 1]);
+    ev0 = ev_used ? ev_pool[0].first : ev0;
+    ev1 = ev_used ? ev_pool[0].second : ev1;
+    ev_used = 0;
+    return CL_OK;
+  }
+  Layout lay{};
+  int32_t s_cap = 0;
+  bool need_fresh = true;
+  DevBuf<Op> d_ops;
+  size_t ops_uploaded = 0;
+  DevBuf<int32_t> d_topo;
+  DevBuf<uint8_t> d_sched;
+  DevBuf<uint32_t> d_state;
+  DevBuf<int32_t> d_regs;
+  DevBuf<int32_t> d_snap_tok;
+  DevBuf<uint32_t> d_snap_rec;
+  DevBuf<int32_t> d_snap_tick;
+  DevBuf<uint32_t> d_ovf;
+  DevBuf<uint32_t> d_ovh;
+  DevBuf<int32_t> d_hist;
+  DevBuf<unsigned long long> d_sums;
+
+  // host mirrors of results (invalidated by every launch)
+  bool h_valid = false;
+  std::vector<int32_t> h_regs, h_snap_tok, h_snap_tick, h_tok;
+  std::vector<uint32_t> h_snap_rec;
+
+  ~cl_sim() {
+    if (dev_ready) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(stream);
+      d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
+      d_snap_tok.release(); d_snap_rec.release(); d_snap_tick.release(); d_ovf.release();
+      d_ovh.release(); d_hist.release(); d_sums.release();
+      for (auto& e : ev_pool) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+      }
+      (void)hipStreamDestroy(stream);
+    }
+  }
+
+  int node_of(const char* id) const {
+    auto it = id_index.find(id ? std::string(id) : std::string());
+    return it == id_index.end() ? -1 : it->second;
+  }
+
+  // Freeze the topology into rank order (getSortedKeys, common.go:135-146).
+  int freeze() {
+    if (frozen) return CL_OK;
+    const int n = (int)ids.size();
+    if (n > kMaxNodes) return set_err(CL_E_LIMIT, "%d nodes exceed the small-graph engine limit %d", n, kMaxNodes);
+    by_rank.resize(n);
+    for (int i = 0; i < n; ++i) by_rank[i] = i;
+    std::sort(by_rank.begin(), by_rank.end(), [&](int a, int b) { return ids[a] < ids[b]; });
+    rank_of.assign(n, 0);
+    for (int r = 0; r < n; ++r) rank_of[by_rank[r]] = r;
+    std::vector<std::pair<int, int>> ch;
+    for (auto& l : links) ch.emplace_back(rank_of[l.first], rank_of[l.second]);
+    std::sort(ch.begin(), ch.end());
+    const int C = (int)ch.size();
+    out_off.assign(n + 1, 0);
+    in_off.assign(n + 1, 0);
+    ch_dst.resize(C);
+    ch_src.resize(C);
+    for (int c = 0; c < C; ++c) {
+      ch_src[c] = ch[c].first;
+      ch_dst[c] = ch[c].second;
+      out_off[ch[c].first + 1]++;
+      in_off[ch[c].second + 1]++;
+    }
+    for (int v = 0; v < n; ++v) {
+      out_off[v + 1] += out_off[v];
+      in_off[v + 1] += in_off[v];
+    }
+    in_ch.resize(C);
+    std::vector<int32_t> fill(in_off.begin(), in_off.end() - 1);
+    for (int c = 0; c < C; ++c) in_ch[fill[ch_dst[c]]++] = c;  // channels sorted by src: in-lists by src rank
+    init_tok.resize(n);
+    total_tokens = 0;
+    for (int r = 0; r < n; ++r) {
+      init_tok[r] = (int32_t)init_tokens[by_rank[r]];
+      total_tokens += init_tokens[by_rank[r]];
+    }
+    hist.assign(C, {});
+    depth_bound.assign(C, 0);
+    frozen = true;
+    return CL_OK;
+  }
+
+  int channel_of(int src_rank, int dst_rank) const {
+    for (int c = out_off[src_rank]; c < out_off[src_rank + 1]; ++c)
+      if (ch_dst[c] == dst_rank) return c;
+    return -1;
+  }
+
+  int64_t draws_needed() const { return sends + (int64_t)n_sids * (int64_t)ch_dst.size(); }
+
+  int ocap_log2_needed() const {
+    int32_t mx = 0;
+    for (auto d : depth_bound) mx = std::max(mx, d);
+    const int32_t cap = 1 << cap_log2;
+    if (mx <= cap) return -1;
+    int need = std::min(mx, kMaxQueued) - cap, l = 0;
+    while ((1 << l) < need) ++l;
+    return l;
+  }
+
+  int ensure_device() {
+    if (dev_ready) return CL_OK;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+      return set_err(CL_E_DEVICE, "no HIP device available (the engine needs a gfx950 GPU)");
+    if (device < 0 || device >= count) return set_err(CL_E_DEVICE, "device %d out of range (%d)", device, count);
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      return set_err(CL_E_DEVICE, "device %d is %s, the engine is built for gfx950", device, prop.gcnArchName);
+    HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    dev_ready = true;
+    return CL_OK;
+  }
+
+  int upload_topology() {
+    const int n = (int)ids.size(), C = (int)ch_dst.size();
+    std::vector<int32_t> t;
+    t.insert(t.end(), out_off.begin(), out_off.end());
+    t.insert(t.end(), ch_dst.begin(), ch_dst.end());
+    t.insert(t.end(), in_off.begin(), in_off.end());
+    t.insert(t.end(), in_ch.begin(), in_ch.end());
+    t.insert(t.end(), init_tok.begin(), init_tok.end());
+    (void)n; (void)C;
+    int rc = d_topo.ensure(t.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(d_topo.p, t.data(), t.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    return CL_OK;
+  }
+
+  int ensure_delays() {
+    int64_t need = draws_needed();
+    if (go_seeds) {
+      int64_t D = std::max<int64_t>(16, (need + 15) / 16 * 16);
+      if (dev_draws >= D) return CL_OK;
+      std::vector<uint8_t> sched((size_t)(D * n_inst));
+      go_schedule(seed_base, n_inst, D, sched.data());
+      int rc = d_sched.ensure(sched.size());
+      if (rc) return rc;
+      HIP_TRY(hipMemcpy(d_sched.p, sched.data(), sched.size(), hipMemcpyHostToDevice));
+      dev_draws = D;  // longer rows of the same streams: saved draw cursors stay valid
+      return CL_OK;
+    }
+    if (dev_draws == user_draws) return CL_OK;
+    int rc = d_sched.ensure(user_sched.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(d_sched.p, user_sched.data(), user_sched.size(), hipMemcpyHostToDevice));
+    dev_draws = user_draws;
+    return CL_OK;
+  }
+
+  // Allocate per-instance state and outputs for the current layout.
+  int ensure_layout() {
+    const int n = (int)ids.size(), C = (int)ch_dst.size();
+    int32_t want_s = std::max<int32_t>(4, (n_sids + 3) / 4 * 4);
+    int ocap = ocap_log2_needed();
+    if (!need_fresh && want_s <= s_cap && ocap <= lay.ocap_log2 && lay.cap_log2 == cap_log2) return CL_OK;
+    s_cap = std::max(want_s, s_cap);
+    if (s_cap > kMaxSnapshots) return set_err(CL_E_LIMIT, "more than %d snapshots", kMaxSnapshots);
+    Layout L = make_layout(n, C, cap_log2, std::max(ocap, lay.words ? lay.ocap_log2 : -1), s_cap);
+    if ((int64_t)L.words * kWave * 4 > kMaxLdsBytes)
+      return set_err(CL_E_LIMIT, "instance state of %d words exceeds LDS (lower fifo slots or graph size)", L.words);
+    lay = L;
+    int rc;
+    if ((rc = d_state.ensure((size_t)lay.words * stride))) return rc;
+    if ((rc = d_regs.ensure((size_t)R_NUM * stride))) return rc;
+    if ((rc = d_snap_tok.ensure((size_t)s_cap * n * stride))) return rc;
+    if ((rc = d_snap_rec.ensure((size_t)s_cap * std::max(C, 1) * stride))) return rc;
+    if ((rc = d_snap_tick.ensure((size_t)s_cap * stride))) return rc;
+    const size_t ov = lay.ocap_log2 >= 0 ? ((size_t)C << lay.ocap_log2) * stride : 1;
+    if ((rc = d_ovf.ensure(ov))) return rc;
+    if ((rc = d_ovh.ensure(lay.ocap_log2 >= 0 ? (size_t)std::max(C, 1) * stride : 1))) return rc;
+    need_fresh = true;
+    return CL_OK;
+  }
+
+  int upload_hist() {
+    std::vector<int32_t> off(1, 0), val;
+    for (auto& h : hist) {
+      val.insert(val.end(), h.begin(), h.end());
+      off.push_back((int32_t)val.size());
+    }
+    std::vector<int32_t> all(off);
+    all.insert(all.end(), val.begin(), val.end());
+    int rc = d_hist.ensure(all.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(d_hist.p, all.data(), all.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    return CL_OK;
+  }
+
+  ExecParams exec_params(int32_t op_begin, int32_t n_started_before) const {
+    ExecParams p{};
+    const int n = (int)ids.size(), C = (int)ch_dst.size();
+    p.op_begin = op_begin;
+    p.op_end = (int32_t)ops.size();
+    p.n_nodes = n;
+    p.n_ch = C;
+    p.lay = lay;
+    p.n_started_before = n_started_before;
+    p.draws = dev_draws;
+    p.n_inst = n_inst;
+    p.stride = stride;
+    p.fresh = op_begin == 0 ? 1 : 0;
+    p.state = d_state.p;
+    p.regs = d_regs.p;
+    p.snap_tok = d_snap_tok.p;
+    p.snap_rec = d_snap_rec.p;
+    p.snap_tick = d_snap_tick.p;
+    p.ovf = d_ovf.p;
+    p.ovh = d_ovh.p;
+    return p;
+  }
+
+  // Launch pending ops (all ops when a fresh replay is needed). Asynchronous.
+  int launch(bool force_fresh) {
+    int rc = freeze();
+    if (rc) return rc;
+    if ((rc = ensure_device())) return rc;
+    HIP_TRY(hipSetDevice(device));
+    if (!d_topo.p && (rc = upload_topology())) return rc;
+    if ((rc = ensure_layout())) return rc;
+    if ((rc = ensure_delays())) return rc;
+    if (force_fresh) need_fresh = true;
+    if (!need_fresh && executed == (int32_t)ops.size()) return CL_OK;
+    if (ops.size() > ops_uploaded || !d_ops.p) {
+      if ((rc = d_ops.ensure(std::max<size_t>(ops.size(), 64)))) return rc;
+      HIP_TRY(hipMemcpy(d_ops.p, ops.data(), ops.size() * sizeof(Op), hipMemcpyHostToDevice));
+      ops_uploaded = ops.size();
+    }
+    int32_t begin = need_fresh ? 0 : executed;
+    int32_t started_before = 0;
+    for (int32_t i = 0; i < begin; ++i) started_before += ops[i].kind == OP_SNAP;
+    if (begin == 0) {
+      HIP_TRY(hipMemsetAsync(d_snap_tick.p, 0xff, d_snap_tick.n * sizeof(int32_t), stream));
+      if (lay.ocap_log2 >= 0) HIP_TRY(hipMemsetAsync(d_ovh.p, 0, d_ovh.n * sizeof(uint32_t), stream));
+    }
+    ExecParams p = exec_params(begin, started_before);
+    if (ev_used == 256 && (rc = fold_events())) return rc;
+    if (ev_used == ev_pool.size()) {
+      std::pair<hipEvent_t, hipEvent_t> pr;
+      HIP_TRY(hipEventCreate(&pr.first));
+      HIP_TRY(hipEventCreate(&pr.second));
+      ev_pool.push_back(pr);
+    }
+    auto& pr = ev_pool[ev_used++];
+    HIP_TRY(hipEventRecord(pr.first, stream));
+    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p, stream);
+    if (e != 0) return set_err(CL_E_DEVICE, "exec kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    HIP_TRY(hipEventRecord(pr.second, stream));
+    ev0 = pr.first;
+    ev1 = pr.second;
+    timed = true;
+    executed = (int32_t)ops.size();
+    need_fresh = false;
+    h_valid = false;
+    return CL_OK;
+  }
+
+  int sync() {
+    if (!dev_ready) return CL_OK;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipStreamSynchronize(stream));
+    return CL_OK;
+  }
+
+  int flush() {
+    if (!frozen || executed != (int32_t)ops.size() || need_fresh) {
+      int rc = launch(false);
+      if (rc) return rc;
+    }
+    return sync();
+  }
+
+  int fetch() {
+    int rc = flush();
+    if (rc) return rc;
+    if (h_valid) return CL_OK;
+    if (!dev_ready) return set_err(CL_E_STATE, "nothing has run on the device yet");
+    const int n = (int)ids.size(), C = (int)ch_dst.size();
+    h_regs.resize((size_t)R_NUM * stride);
+    h_snap_tok.resize((size_t)s_cap * n * stride);
+    h_snap_rec.resize((size_t)s_cap * std::max(C, 1) * stride);
+    h_snap_tick.resize((size_t)s_cap * stride);
+    h_tok.resize((size_t)n * stride);
+    HIP_TRY(hipMemcpy(h_regs.data(), d_regs.p, h_regs.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(h_snap_tok.data(), d_snap_tok.p, h_snap_tok.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(h_snap_rec.data(), d_snap_rec.p, h_snap_rec.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(h_snap_tick.data(), d_snap_tick.p, h_snap_tick.size() * 4, hipMemcpyDeviceToHost));
+    if (n) HIP_TRY(hipMemcpy(h_tok.data(), d_state.p + (size_t)lay.w_tok * stride, h_tok.size() * 4,
+                             hipMemcpyDeviceToHost));
+    h_valid = true;
+    return CL_OK;
+  }
+
+  int append(Op op) {
+    int rc = freeze();
+    if (rc) return rc;
+    ops.push_back(op);
+    return CL_OK;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char* cl_last_error(void) { return g_last_error.c_str(); }
+
+const char* cl_status_string(int32_t code) {
+  switch (code) {
+    case CL_INST_OK: return "ok";
+    case CL_INST_FATAL_INSUFFICIENT_TOKENS: return "fatal: insufficient tokens (node.go:113-116)";
+    case CL_INST_FATAL_UNKNOWN_DEST: return "fatal: unknown dest (node.go:121-124)";
+    case CL_INST_FIFO_OVERFLOW: return "fifo overflow (engine limit)";
+    case CL_INST_HANG: return "hang: snapshot never completed";
+    case CL_INST_DELAY_EXHAUSTED: return "delay schedule exhausted";
+    default: return "unknown";
+  }
+}
+
+#define SIM_CHECK(s)                                               \
+  do {                                                             \
+    if (!(s)) return set_err(CL_E_INVALID, "null cl_sim handle"); \
+  } while (0)
+
+int cl_sim_create(int64_t n_instances, cl_sim** out) {
+  if (!out || n_instances <= 0) return set_err(CL_E_INVALID, "n_instances must be > 0");
+  cl_sim* s = new cl_sim();
+  s->n_inst = n_instances;
+  s->stride = (n_instances + kWave - 1) / kWave * kWave;
+  *out = s;
+  return CL_OK;
+}
+
+int cl_sim_destroy(cl_sim* sim) {
+  delete sim;
+  return CL_OK;
+}
+
+int cl_add_node(cl_sim* sim, const char* id, int64_t tokens) {
+  SIM_CHECK(sim);
+  if (!id) return set_err(CL_E_INVALID, "null id");
+  if (sim->frozen) return set_err(CL_E_STATE, "AddNode after events started is not supported");
+  if (sim->node_of(id) >= 0) return set_err(CL_E_DUPLICATE_NODE, "node %s already exists", id);
+  if (tokens < INT32_MIN || tokens > INT32_MAX) return set_err(CL_E_LIMIT, "token count out of int32 range");
+  sim->id_index[id] = (int)sim->ids.size();
+  sim->ids.emplace_back(id);
+  sim->init_tokens.push_back(tokens);
+  int64_t total = 0;
+  for (auto t : sim->init_tokens) total += t;
+  if (total > INT32_MAX || total < INT32_MIN) return set_err(CL_E_LIMIT, "total tokens out of int32 range");
+  return CL_OK;
+}
+
+int cl_add_link(cl_sim* sim, const char* src, const char* dest) {
+  SIM_CHECK(sim);
+  const int a = sim->node_of(src), b = sim->node_of(dest);
+  if (a < 0) return set_err(CL_E_UNKNOWN_NODE, "Node %s does not exist", src ? src : "(null)");
+  if (b < 0) return set_err(CL_E_UNKNOWN_NODE, "Node %s does not exist", dest ? dest : "(null)");
+  if (sim->frozen) return set_err(CL_E_STATE, "AddLink after events started is not supported");
+  if (a == b) return CL_OK;  // node.go:88-90
+  for (auto& l : sim->links)
+    if (l.first == a && l.second == b) return CL_OK;  // replacement of an empty queue
+  sim->links.emplace_back(a, b);
+  return CL_OK;
+}
+
+int cl_read_topology_text(cl_sim* sim, const char* text) {
+  SIM_CHECK(sim);
+  if (!text) return set_err(CL_E_INVALID, "null text");
+  int64_t left = -1;
+  for (const std::string& line : go_lines(text)) {
+    if (!line.empty() && line[0] == '#') continue;
+    if (left < 0) {
+      if (!go_atoi(line, &left)) return set_err(CL_E_PARSE, "bad node count line: %s", line.c_str());
+      continue;
+    }
+    auto f = go_fields(line);
+    if (f.size() != 2) return set_err(CL_E_PARSE, "Expected 2 tokens in line: %s", line.c_str());
+    int rc;
+    if (left > 0) {
+      int64_t tok;
+      if (!go_atoi(f[1], &tok)) return set_err(CL_E_PARSE, "bad token count: %s", f[1].c_str());
+      if ((rc = cl_add_node(sim, f[0].c_str(), tok))) return rc;
+      left--;
+    } else if ((rc = cl_add_link(sim, f[0].c_str(), f[1].c_str()))) {
+      return rc;
+    }
+  }
+  return CL_OK;
+}
+
+int cl_read_topology_file(cl_sim* sim, const char* path) {
+  SIM_CHECK(sim);
+  std::string text;
+  if (!path || !read_file(path, &text)) return set_err(CL_E_IO, "cannot read %s", path ? path : "(null)");
+  return cl_read_topology_text(sim, text.c_str());
+}
+
+int cl_set_device(cl_sim* sim, int32_t device_ordinal) {
+  SIM_CHECK(sim);
+  if (sim->dev_ready) return set_err(CL_E_STATE, "device already selected");
+  sim->device = device_ordinal;
+  return CL_OK;
+}
+
+int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks) {
+  SIM_CHECK(sim);
+  int l = 0;
+  while ((1 << l) < fifo_lds_slots) ++l;
+  if (fifo_lds_slots < 2 || fifo_lds_slots > 64 || (1 << l) != fifo_lds_slots)
+    return set_err(CL_E_INVALID, "fifo_lds_slots must be a power of two in [2, 64]");
+  if (max_drain_ticks < 0) return set_err(CL_E_INVALID, "max_drain_ticks must be >= 0");
+  if (l != sim->cap_log2) sim->need_fresh = true;
+  sim->cap_log2 = l;
+  sim->max_drain = max_drain_ticks;
+  return CL_OK;
+}
+
+int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
+  SIM_CHECK(sim);
+  sim->go_seeds = true;
+  sim->seed_base = seed_base;
+  sim->dev_draws = -1;
+  sim->need_fresh = true;
+  return CL_OK;
+}
+
+int cl_set_delay_schedule(cl_sim* sim, const uint8_t* delays, int64_t draws_per_instance) {
+  SIM_CHECK(sim);
+  if (!delays || draws_per_instance <= 0) return set_err(CL_E_INVALID, "empty schedule");
+  const size_t n = (size_t)(draws_per_instance * sim->n_inst);
+  for (size_t i = 0; i < n; ++i)
+    if (delays[i] >= 5) return set_err(CL_E_INVALID, "delay %u at %zu outside [0, maxDelay)", delays[i], i);
+  sim->user_sched.assign(delays, delays + n);
+  sim->user_draws = draws_per_instance;
+  sim->go_seeds = false;
+  sim->dev_draws = -1;
+  sim->need_fresh = true;
+  return CL_OK;
+}
+
+int cl_send_tokens(cl_sim* sim, const char* src, const char* dest, int64_t n) {
+  SIM_CHECK(sim);
+  int rc = sim->freeze();
+  if (rc) return rc;
+  const int a = sim->node_of(src);
+  if (a < 0) return set_err(CL_E_UNKNOWN_NODE, "send from unknown node %s", src ? src : "(null)");
+  if (n < 0 || n > kMaxPayload) return set_err(CL_E_LIMIT, "token count %lld outside [0, %d]", (long long)n, kMaxPayload);
+  const int b = sim->node_of(dest);
+  const int ra = sim->rank_of[a];
+  const int c = b < 0 ? -1 : sim->channel_of(ra, sim->rank_of[b]);
+  if (c >= 0) {
+    if ((int64_t)sim->hist[c].size() >= kMaxChannelTokens)
+      return set_err(CL_E_LIMIT, "more than %d token messages on one channel", kMaxChannelTokens);
+    sim->hist[c].push_back((int32_t)n);
+    sim->depth_bound[c]++;
+  }
+  sim->sends++;
+  return sim->append(Op{OP_SEND, ra, c, (int32_t)n});
+}
+
+int cl_start_snapshot(cl_sim* sim, const char* node, int32_t* out_sid) {
+  SIM_CHECK(sim);
+  int rc = sim->freeze();
+  if (rc) return rc;
+  const int a = sim->node_of(node);
+  if (a < 0) return set_err(CL_E_UNKNOWN_NODE, "snapshot at unknown node %s", node ? node : "(null)");
+  if (sim->n_sids >= kMaxSnapshots) return set_err(CL_E_LIMIT, "more than %d snapshots", kMaxSnapshots);
+  const int32_t sid = sim->n_sids++;
+  for (auto& d : sim->depth_bound) d++;
+  if (out_sid) *out_sid = sid;
+  return sim->append(Op{OP_SNAP, sim->rank_of[a], sid, 0});
+}
+
+int cl_tick(cl_sim* sim, int32_t n) {
+  SIM_CHECK(sim);
+  int rc = sim->freeze();
+  if (rc) return rc;
+  if (n <= 0) return CL_OK;  // for i := 0; i < numTicks; ... (test_common.go:115)
+  if (sim->time_bound + n > kMaxTime)
+    return set_err(CL_E_LIMIT, "simulated time would exceed %d ticks", kMaxTime);
+  sim->time_bound += n;
+  if (!sim->ops.empty() && sim->ops.back().kind == OP_TICK && sim->executed < (int32_t)sim->ops.size()) {
+    sim->ops.back().a += n;  // merge consecutive ticks of one pending run
+    return CL_OK;
+  }
+  return sim->append(Op{OP_TICK, n, 0, 0});
+}
+
+int cl_drain(cl_sim* sim) {
+  SIM_CHECK(sim);
+  int rc = sim->freeze();
+  if (rc) return rc;
+  const int64_t extra = 6;  // maxDelay + 1 (test_common.go:135-137)
+  int64_t room = kMaxTime - sim->time_bound - extra;
+  if (room < 0) return set_err(CL_E_LIMIT, "simulated time would exceed %d ticks", kMaxTime);
+  const int64_t cap = std::min(sim->max_drain, room);
+  sim->time_bound += cap + extra;
+  return sim->append(Op{OP_DRAIN, (int32_t)cap, (int32_t)extra, 0});
+}
+
+int cl_read_events_text(cl_sim* sim, const char* text, int32_t* n_snapshots) {
+  SIM_CHECK(sim);
+  if (!text) return set_err(CL_E_INVALID, "null text");
+  int32_t snaps = 0;
+  for (const std::string& line : go_lines(text)) {
+    if (line == "#") continue;  // strings.HasPrefix("#", line) (test_common.go:90, sic)
+    auto f = go_fields(line);
+    if (f.empty()) return set_err(CL_E_PARSE, "empty event line");
+    int rc;
+    if (f[0] == "send") {
+      int64_t n;
+      if (f.size() < 4 || !go_atoi(f[3], &n)) return set_err(CL_E_PARSE, "bad send line: %s", line.c_str());
+      rc = cl_send_tokens(sim, f[1].c_str(), f[2].c_str(), n);
+    } else if (f[0] == "snapshot") {
+      if (f.size() < 2) return set_err(CL_E_PARSE, "bad snapshot line: %s", line.c_str());
+      snaps++;
+      rc = cl_start_snapshot(sim, f[1].c_str(), nullptr);
+    } else if (f[0] == "tick") {
+      int64_t n = 1;
+      if (f.size() > 1 && !go_atoi(f[1], &n)) return set_err(CL_E_PARSE, "bad tick line: %s", line.c_str());
+      if (n > INT32_MAX) return set_err(CL_E_LIMIT, "tick count too large");
+      rc = cl_tick(sim, (int32_t)std::max<int64_t>(n, 0));
+    } else {
+      return set_err(CL_E_PARSE, "Unknown event command: %s", f[0].c_str());
+    }
+    if (rc) return rc;
+  }
+  if (n_snapshots) *n_snapshots = snaps;
+  return cl_drain(sim);
+}
+
+int cl_read_events_file(cl_sim* sim, const char* path, int32_t* n_snapshots) {
+  SIM_CHECK(sim);
+  std::string text;
+  if (!path || !read_file(path, &text)) return set_err(CL_E_IO, "cannot read %s", path ? path : "(null)");
+  return cl_read_events_text(sim, text.c_str(), n_snapshots);
+}
+
+int cl_flush(cl_sim* sim) {
+  SIM_CHECK(sim);
+  return sim->flush();
+}
+
+int cl_rerun(cl_sim* sim) {
+  SIM_CHECK(sim);
+  return sim->launch(true);
+}
+
+int cl_synchronize(cl_sim* sim) {
+  SIM_CHECK(sim);
+  return sim->sync();
+}
+
+int cl_last_kernel_ms(cl_sim* sim, double* ms) {
+  SIM_CHECK(sim);
+  if (!ms) return set_err(CL_E_INVALID, "null output");
+  if (!sim->timed) return set_err(CL_E_STATE, "no kernel has run");
+  int rc = sim->sync();
+  if (rc) return rc;
+  float f = 0.f;
+  HIP_TRY(hipEventElapsedTime(&f, sim->ev0, sim->ev1));
+  *ms = f;
+  return CL_OK;
+}
+
+int cl_kernel_time(cl_sim* sim, double* total_ms, int64_t* launches) {
+  SIM_CHECK(sim);
+  if (!total_ms || !launches) return set_err(CL_E_INVALID, "null output");
+  int rc = sim->sync();
+  if (rc) return rc;
+  if (sim->dev_ready && (rc = sim->fold_events())) return rc;
+  *total_ms = sim->ev_folded_ms;
+  *launches = sim->ev_folded_n;
+  sim->ev_folded_ms = 0;
+  sim->ev_folded_n = 0;
+  return CL_OK;
+}
+
+int cl_num_nodes(const cl_sim* sim, int32_t* n) {
+  SIM_CHECK(sim);
+  *n = (int32_t)sim->ids.size();
+  return CL_OK;
+}
+
+int cl_node_id(const cl_sim* sim, int32_t rank, const char** id) {
+  SIM_CHECK(sim);
+  if (!sim->frozen) {
+    int rc = const_cast<cl_sim*>(sim)->freeze();
+    if (rc) return rc;
+  }
+  if (rank < 0 || rank >= (int32_t)sim->ids.size()) return set_err(CL_E_INVALID, "rank out of range");
+  *id = sim->ids[sim->by_rank[rank]].c_str();
+  return CL_OK;
+}
+
+int cl_num_channels(const cl_sim* sim, int32_t* n) {
+  SIM_CHECK(sim);
+  *n = (int32_t)sim->links.size();
+  return CL_OK;
+}
+
+int cl_channel(const cl_sim* sim, int32_t ch, int32_t* src_rank, int32_t* dest_rank) {
+  SIM_CHECK(sim);
+  if (!sim->frozen) {
+    int rc = const_cast<cl_sim*>(sim)->freeze();
+    if (rc) return rc;
+  }
+  if (ch < 0 || ch >= (int32_t)sim->ch_dst.size()) return set_err(CL_E_INVALID, "channel out of range");
+  *src_rank = sim->ch_src[ch];
+  *dest_rank = sim->ch_dst[ch];
+  return CL_OK;
+}
+
+int cl_num_snapshots(const cl_sim* sim, int32_t* n) {
+  SIM_CHECK(sim);
+  *n = sim->n_sids;
+  return CL_OK;
+}
+
+int cl_num_instances(const cl_sim* sim, int64_t* n) {
+  SIM_CHECK(sim);
+  *n = sim->n_inst;
+  return CL_OK;
+}
+
+int cl_delay_draws_needed(const cl_sim* sim, int64_t* draws) {
+  SIM_CHECK(sim);
+  *draws = sim->draws_needed();
+  return CL_OK;
+}
+
+int cl_device_bytes(const cl_sim* sim, int64_t* bytes) {
+  SIM_CHECK(sim);
+  int64_t b = 0;
+  b += sim->d_ops.n * sizeof(Op) + sim->d_topo.n * 4 + sim->d_sched.n + sim->d_state.n * 4 + sim->d_regs.n * 4;
+  b += sim->d_snap_tok.n * 4 + sim->d_snap_rec.n * 4 + sim->d_snap_tick.n * 4 + sim->d_ovf.n * 4;
+  b += sim->d_ovh.n * 4 + sim->d_hist.n * 4 + sim->d_sums.n * 8;
+  *bytes = b;
+  return CL_OK;
+}
+
+int cl_get_status(cl_sim* sim, int32_t* out) {
+  SIM_CHECK(sim);
+  int rc = sim->fetch();
+  if (rc) return rc;
+  std::memcpy(out, sim->h_regs.data() + (size_t)R_STATUS * sim->stride, sim->n_inst * 4);
+  return CL_OK;
+}
+
+int cl_get_time(cl_sim* sim, int32_t* out) {
+  SIM_CHECK(sim);
+  int rc = sim->fetch();
+  if (rc) return rc;
+  std::memcpy(out, sim->h_regs.data() + (size_t)R_TIME * sim->stride, sim->n_inst * 4);
+  return CL_OK;
+}
+
+int cl_node_tokens(cl_sim* sim, int64_t inst, int64_t* out) {
+  SIM_CHECK(sim);
+  if (inst < 0 || inst >= sim->n_inst) return set_err(CL_E_INVALID, "instance out of range");
+  int rc = sim->fetch();
+  if (rc) return rc;
+  for (size_t r = 0; r < sim->ids.size(); ++r) out[r] = sim->h_tok[r * sim->stride + inst];
+  return CL_OK;
+}
+
+int cl_snapshot_tick(cl_sim* sim, int32_t sid, int64_t inst, int32_t* tick) {
+  SIM_CHECK(sim);
+  if (inst < 0 || inst >= sim->n_inst || sid < 0 || sid >= sim->n_sids)
+    return set_err(CL_E_INVALID, "snapshot/instance out of range");
+  int rc = sim->fetch();
+  if (rc) return rc;
+  *tick = sim->h_snap_tick[(size_t)sid * sim->stride + inst];
+  return CL_OK;
+}
+
+int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens, int64_t* msg_offsets,
+                        int64_t* msg_tokens, int64_t msg_cap) {
+  SIM_CHECK(sim);
+  if (inst < 0 || inst >= sim->n_inst || sid < 0 || sid >= sim->n_sids)
+    return set_err(CL_E_INVALID, "snapshot/instance out of range");
+  int rc = sim->fetch();
+  if (rc) return rc;
+  const size_t st = sim->stride;
+  if (sim->h_snap_tick[(size_t)sid * st + inst] < 0)
+    return set_err(CL_E_NOT_COMPLETE, "snapshot %d has not completed in instance %lld", sid, (long long)inst);
+  const int n = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
+  for (int v = 0; v < n; ++v) tokens[v] = sim->h_snap_tok[((size_t)sid * n + v) * st + inst];
+  int64_t m = 0;
+  bool fits = true;
+  for (int c = 0; c < C; ++c) {
+    msg_offsets[c] = m;
+    const uint32_t rec = sim->h_snap_rec[((size_t)sid * C + c) * st + inst];
+    const uint32_t b = rec & 0xffffu, e = rec >> 16;
+    for (uint32_t k = b; k < e; ++k, ++m) {
+      if (m < msg_cap) msg_tokens[m] = sim->hist[c][k];
+      else fits = false;
+    }
+  }
+  msg_offsets[C] = m;
+  return fits ? CL_OK : set_err(CL_E_LIMIT, "msg_cap %lld < %lld messages", (long long)msg_cap, (long long)m);
+}
+
+int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out) {
+  SIM_CHECK(sim);
+  int rc = sim->fetch();
+  if (rc) return rc;
+  for (int k = 0; k < CL_NUM_COUNTERS; ++k) out[k] = 0;
+  const size_t st = sim->stride;
+  const int C = (int)sim->ch_dst.size();
+  const int32_t* R = sim->h_regs.data();
+  for (int64_t i = 0; i < sim->n_inst; ++i) {
+    if (only_ok && R[R_STATUS * st + i] != ST_OK) continue;
+    out[CL_CNT_PUSH] += (uint32_t)R[R_PUSH * st + i];
+    out[CL_CNT_PEEK] += (uint32_t)R[R_PEEK * st + i];
+    out[CL_CNT_POP_TOKEN] += (uint32_t)R[R_POP_TOK * st + i];
+    out[CL_CNT_POP_MARKER] += (uint32_t)R[R_POP_MK * st + i];
+    out[CL_CNT_COMPLETED] += R[R_NDONE * st + i];
+    out[CL_CNT_INSTANCES] += 1;
+    out[CL_CNT_TICKS] += R[R_TIME * st + i];
+    for (int32_t s = 0; s < sim->n_sids; ++s) {
+      if (sim->h_snap_tick[(size_t)s * st + i] < 0) continue;
+      for (int c = 0; c < C; ++c) {
+        const uint32_t rec = sim->h_snap_rec[((size_t)s * C + c) * st + i];
+        out[CL_CNT_RECORDED] += (rec >> 16) - (rec & 0xffffu);
+      }
+    }
+  }
+  return CL_OK;
+}
+
+int cl_get_checksums(cl_sim* sim, int64_t* out) {
+  SIM_CHECK(sim);
+  int rc = sim->flush();
+  if (rc) return rc;
+  if (!sim->dev_ready) return set_err(CL_E_STATE, "nothing has run on the device yet");
+  HIP_TRY(hipSetDevice(sim->device));
+  if ((rc = sim->upload_hist())) return rc;
+  if ((rc = sim->d_sums.ensure(CL_NUM_SUMS))) return rc;
+  HIP_TRY(hipMemsetAsync(sim->d_sums.p, 0, CL_NUM_SUMS * sizeof(unsigned long long), sim->stream));
+  SumParams p{};
+  p.n_nodes = (int32_t)sim->ids.size();
+  p.n_ch = (int32_t)sim->ch_dst.size();
+  p.s_cap = sim->s_cap;
+  p.n_sids = sim->n_sids;
+  p.n_inst = sim->n_inst;
+  p.stride = sim->stride;
+  p.regs = sim->d_regs.p;
+  p.snap_tok = sim->d_snap_tok.p;
+  p.snap_rec = sim->d_snap_rec.p;
+  p.snap_tick = sim->d_snap_tick.p;
+  p.state = sim->d_state.p;
+  p.lay = sim->lay;
+  p.hist_off = sim->d_hist.p;
+  p.hist_val = sim->d_hist.p + sim->hist.size() + 1;
+  p.total_tokens = sim->total_tokens;
+  p.out = sim->d_sums.p;
+  int e = launch_checksums(p, sim->stream);
+  if (e) return set_err(CL_E_DEVICE, "checksum kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+  unsigned long long h[CL_NUM_SUMS];
+  HIP_TRY(hipMemcpyAsync(h, sim->d_sums.p, sizeof h, hipMemcpyDeviceToHost, sim->stream));
+  HIP_TRY(hipStreamSynchronize(sim->stream));
+  for (int k = 0; k < CL_NUM_SUMS; ++k) out[k] = (int64_t)h[k];
+  return CL_OK;
+}
+
+int cl_go_delay_schedule(int64_t seed_base, int64_t n, int64_t draws, uint8_t* out) {
+  if (!out || n < 0 || draws < 0) return set_err(CL_E_INVALID, "bad arguments");
+  go_schedule(seed_base, n, draws, out);
+  return CL_OK;
+}
+
+int cl_go_int63(int64_t seed, int64_t n, int64_t* out) {
+  if (!out || n < 0) return set_err(CL_E_INVALID, "bad arguments");
+  GoRand r(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = r.int63();
+  return CL_OK;
+}
+
+int cl_go_intn(int64_t seed, int32_t bound, int64_t n, int32_t* out) {
+  if (!out || n < 0 || bound <= 0) return set_err(CL_E_INVALID, "bad arguments");
+  GoRand r(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = r.int31n(bound);
+  return CL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,183 @@
+/*
+ * clsnap.h -- C ABI of the MI355X Chandy-Lamport batch engine.
+ *
+ * One cl_sim is a batch of n_instances independent copies of the reference simulator
+ * (sim.go ChandyLamportSim).  Every instance shares the topology and receives the same
+ * event stream (send / snapshot / tick), but draws its own per-message delays, so each
+ * instance is the reference run under its own delay stream.  Instances run as
+ * tick-synchronous simulations on one gfx950 GPU; results are bit-exact per instance.
+ *
+ * Each entry point below names the reference interface it replaces
+ * (paths relative to /root/reference/chandy_lamport).  The reference is a Go package
+ * with no FFI; INTEGRATION.md shows the cgo binding that maps this ABI back onto the
+ * reference's Simulator API so the .top/.events drivers and snapshot_test.go run
+ * unchanged.
+ *
+ * Conventions
+ *   - Every call returns int: CL_OK (0) or a negative CL_E_* code; cl_last_error()
+ *     describes the most recent failure on the calling thread.
+ *   - All buffers are caller-allocated; no pointer returned by the library is owned by
+ *     the caller except where stated.
+ *   - One host thread drives a cl_sim.  Event calls only append to the sim's event
+ *     program; cl_flush() (or any result query) executes pending events on the GPU.
+ *   - Node order everywhere is the reference's getSortedKeys order (common.go:135-146):
+ *     lexicographic byte order of the node IDs ("rank").  Channel c is the c-th link in
+ *     (src rank, dest rank) order -- the order Tick scans senders and out-links
+ *     (sim.go:76-78).
+ *   - Where the reference calls log.Fatal* on a per-run condition, the affected
+ *     instance gets a CL_INST_* status and freezes; API misuse that the reference
+ *     turns into a process exit or nil dereference returns a CL_E_* code instead.
+ */
+#ifndef CLSNAP_H
+#define CLSNAP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ------------------------------------------------------- */
+#define CL_OK 0
+#define CL_E_INVALID (-1)        /* bad argument or handle */
+#define CL_E_UNKNOWN_NODE (-2)   /* sim.go:49-54 log.Fatalf; nil *Node at sim.go:61,106 */
+#define CL_E_DUPLICATE_NODE (-3) /* sim.go:42 would silently replace a wired node */
+#define CL_E_PARSE (-4)          /* test_common.go parse fatals (:45,52,58,93,119,...) */
+#define CL_E_IO (-5)             /* ioutil.ReadFile failure (test_common.go:30,80) */
+#define CL_E_DEVICE (-6)         /* HIP error or no gfx950 device */
+#define CL_E_LIMIT (-7)          /* engine limit (nodes, snapshots, token range) */
+#define CL_E_STATE (-8)          /* topology change after events started, etc. */
+#define CL_E_NOT_COMPLETE (-9)   /* collect of a snapshot that has not completed */
+
+/* ---- per-instance status (cl_get_status) -------------------------------- */
+#define CL_INST_OK 0
+#define CL_INST_FATAL_INSUFFICIENT_TOKENS 1 /* node.go:113-116 */
+#define CL_INST_FATAL_UNKNOWN_DEST 2        /* node.go:121-124 */
+#define CL_INST_FIFO_OVERFLOW 3             /* engine: channel deeper than 255 packets */
+#define CL_INST_HANG 4                      /* drain exceeded max ticks (test_common.go:124-132 loops forever) */
+#define CL_INST_DELAY_EXHAUSTED 5           /* replayed delay schedule too short */
+
+/* ---- counters (cl_get_counters), summed over instances ------------------ */
+#define CL_CNT_PUSH 0      /* Queue.Push (queue.go:18) == delay draws (sim.go:101) */
+#define CL_CNT_PEEK 1      /* Queue.Peek inside Tick (sim.go:83) */
+#define CL_CNT_POP_TOKEN 2 /* delivered token packets (sim.go:85) */
+#define CL_CNT_POP_MARKER 3
+#define CL_CNT_RECORDED 4  /* recorded message copies (node.go:179-183) */
+#define CL_CNT_COMPLETED 5 /* globally completed snapshots (sim.go:126-131) */
+#define CL_CNT_INSTANCES 6 /* instances counted */
+#define CL_CNT_TICKS 7     /* sum of per-instance simulator time */
+#define CL_NUM_COUNTERS 8
+
+/* ---- checksums (cl_get_checksums): int64 sums, all-reducible across ranks -- */
+#define CL_SUM_INSTANCES 0       /* instances in the batch */
+#define CL_SUM_OK 1              /* status OK */
+#define CL_SUM_FATAL 2           /* FATAL_* statuses */
+#define CL_SUM_OTHER 3           /* FIFO_OVERFLOW / HANG / DELAY_EXHAUSTED */
+#define CL_SUM_DELIVERED 4       /* packets delivered by OK instances */
+#define CL_SUM_SNAPSHOT_HASH 5   /* sum of snapshot content hashes over OK instances */
+#define CL_SUM_CUT_RESIDUAL 6    /* sum |snapshot tokens + recorded - total| (0 = consistent cuts) */
+#define CL_SUM_FINAL_RESIDUAL 7  /* sum |final tokens + in-flight tokens - total| (checkTokens) */
+#define CL_SUM_COMPLETED 8       /* completed snapshots over OK instances */
+#define CL_SUM_IN_FLIGHT 9       /* token packets still queued at the end (OK instances) */
+#define CL_NUM_SUMS 10
+
+typedef struct cl_sim cl_sim;
+
+/* NewSimulator (sim.go:28-37) for n_instances independent instances. No GPU work. */
+int cl_sim_create(int64_t n_instances, cl_sim** out);
+int cl_sim_destroy(cl_sim* sim);
+
+/* AddNode (sim.go:40-43; node.go:45-55). Token counts must fit int32 in total. */
+int cl_add_node(cl_sim* sim, const char* id, int64_t tokens);
+/* AddLink (sim.go:46-56; node.go:87-94): self links ignored, duplicates replace. */
+int cl_add_link(cl_sim* sim, const char* src, const char* dest);
+/* readTopologyFile (test_common.go:29-68) on a file path / on text. */
+int cl_read_topology_file(cl_sim* sim, const char* path);
+int cl_read_topology_text(cl_sim* sim, const char* text);
+
+/* Engine configuration (before the first flush). */
+int cl_set_device(cl_sim* sim, int32_t device_ordinal);
+/* fifo_lds_slots: per-channel packets kept in LDS (power of two, 2..64; deeper
+ * channels spill to HBM).  max_drain_ticks bounds the drain loop (HANG status). */
+int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks);
+
+/* Delay source replacing rand.Intn(maxDelay) at sim.go:101.
+ * Go stream: instance i draws from rand.Seed(seed_base + i) -- the reference's own
+ * generator (snapshot_test.go:20), restated bit-exactly and precomputed on the host. */
+int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base);
+/* Explicit schedule: delays[i * draws_per_instance + k] in [0, 5) is the k-th draw
+ * of instance i.  Copied; the caller may free it after the call. */
+int cl_set_delay_schedule(cl_sim* sim, const uint8_t* delays, int64_t draws_per_instance);
+
+/* ProcessEvent(PassTokenEvent) -> SendTokens (sim.go:58-62; node.go:112-131). */
+int cl_send_tokens(cl_sim* sim, const char* src, const char* dest, int64_t n);
+/* ProcessEvent(SnapshotEvent) -> StartSnapshot (sim.go:63-64,105-123). */
+int cl_start_snapshot(cl_sim* sim, const char* node, int32_t* out_sid);
+/* Tick (sim.go:71-95), n times. */
+int cl_tick(cl_sim* sim, int32_t n);
+/* The drain of readEventsFile (test_common.go:123-137): tick until every started
+ * snapshot has completed in an instance, then maxDelay+1 more ticks (per instance). */
+int cl_drain(cl_sim* sim);
+/* readEventsFile (test_common.go:79-140) incl. the drain; n_snapshots may be NULL. */
+int cl_read_events_file(cl_sim* sim, const char* path, int32_t* n_snapshots);
+int cl_read_events_text(cl_sim* sim, const char* text, int32_t* n_snapshots);
+
+/* Execute pending events on the GPU and wait. */
+int cl_flush(cl_sim* sim);
+/* Re-run the whole event program from the initial topology state (asynchronous on
+ * the sim's stream; inputs stay resident in HBM).  cl_synchronize() waits. */
+int cl_rerun(cl_sim* sim);
+int cl_synchronize(cl_sim* sim);
+/* Device time of the most recent cl_flush/cl_rerun kernel, from HIP events on the
+ * stream the kernel runs on. */
+int cl_last_kernel_ms(cl_sim* sim, double* ms);
+/* Sum of exec-kernel device times (HIP events around every launch) since the previous
+ * call, and the number of launches; resets the accumulator. */
+int cl_kernel_time(cl_sim* sim, double* total_ms, int64_t* launches);
+
+/* ---- topology queries (host only) ---------------------------------------- */
+int cl_num_nodes(const cl_sim* sim, int32_t* n);
+int cl_node_id(const cl_sim* sim, int32_t rank, const char** id); /* owned by sim */
+int cl_num_channels(const cl_sim* sim, int32_t* n);
+int cl_channel(const cl_sim* sim, int32_t ch, int32_t* src_rank, int32_t* dest_rank);
+int cl_num_snapshots(const cl_sim* sim, int32_t* n);
+int cl_num_instances(const cl_sim* sim, int64_t* n);
+/* Delay draws per instance the current event program can consume (upper bound). */
+int cl_delay_draws_needed(const cl_sim* sim, int64_t* draws);
+/* Bytes of GPU memory the batch holds (after flush). */
+int cl_device_bytes(const cl_sim* sim, int64_t* bytes);
+
+/* ---- results (flush pending events first) -------------------------------- */
+int cl_get_status(cl_sim* sim, int32_t* out /* [n_instances] */);
+int cl_get_time(cl_sim* sim, int32_t* out /* [n_instances] */);
+/* Final node tokens (checkTokens, test_common.go:298-302), rank order. */
+int cl_node_tokens(cl_sim* sim, int64_t inst, int64_t* out /* [num_nodes] */);
+/* Completion tick of snapshot sid in instance inst, -1 if not complete. */
+int cl_snapshot_tick(cl_sim* sim, int32_t sid, int64_t inst, int32_t* tick);
+/* CollectSnapshot (sim.go:134-173) of one instance: tokens[rank] = tokenMap, and the
+ * recorded messages as a CSR over channels: messages of channel c are
+ * msg_tokens[msg_offsets[c] .. msg_offsets[c+1]) in delivery order.  Returns
+ * CL_E_NOT_COMPLETE if the snapshot has not completed in that instance; if msg_cap is
+ * too small, offsets are still written and CL_E_LIMIT is returned. */
+int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens,
+                        int64_t* msg_offsets /* [num_channels + 1] */, int64_t* msg_tokens,
+                        int64_t msg_cap);
+/* Counters over instances (only_ok: restrict to CL_INST_OK instances). */
+int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out /* [CL_NUM_COUNTERS] */);
+/* Batch checksums computed on the GPU (see CL_SUM_*); all-reduce them across ranks. */
+int cl_get_checksums(cl_sim* sim, int64_t* out /* [CL_NUM_SUMS] */);
+
+/* ---- delay-stream utility (host only) ------------------------------------ */
+/* out[i*draws + k] = k-th rand.Intn(5) of rand.Seed(seed_base + i), i in [0, n). */
+int cl_go_delay_schedule(int64_t seed_base, int64_t n, int64_t draws, uint8_t* out);
+/* Go math/rand Int63 / Intn restatement, for known-answer tests. */
+int cl_go_int63(int64_t seed, int64_t n, int64_t* out);
+int cl_go_intn(int64_t seed, int32_t bound, int64_t n, int32_t* out);
+
+const char* cl_status_string(int32_t code);
+const char* cl_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLSNAP_H */

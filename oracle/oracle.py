@@ -55,8 +55,8 @@ def lib():
             "orc_snapshot_hash": (C.c_uint64, [vp, C.c_int]),
             "orc_read_topology": (C.c_int, [vp, cp]),
             "orc_read_events": (C.c_int, [vp, cp, i64]),
-            "orc_read_topology_text": (C.c_int, [vp, cp]),
-            "orc_read_events_text": (C.c_int, [vp, cp, i64]),
+            "orc_read_topology_text": (C.c_int, [vp, vp]),
+            "orc_read_events_text": (C.c_int, [vp, vp, i64]),
             "orc_go_int63_seq": (None, [i64, i64, vp]),
             "orc_go_intn_seq": (None, [i64, i32, i64, vp]),
             "orc_run_batch": (C.c_double, [cp, cp, i64, vp, i64, i64, i64, C.c_int,
@@ -140,6 +140,14 @@ class OracleSim:
 
     def read_events(self, path, max_drain=MAX_DRAIN_TICKS):
         return self._L.orc_read_events(self._h, path.encode(), max_drain)
+
+    def read_topology_text(self, text):
+        buf = C.create_string_buffer(text.encode())   # the C parser tokenizes in place
+        return self._L.orc_read_topology_text(self._h, buf)
+
+    def read_events_text(self, text, max_drain=MAX_DRAIN_TICKS):
+        buf = C.create_string_buffer(text.encode())
+        return self._L.orc_read_events_text(self._h, buf, max_drain)
 
     @property
     def status(self):

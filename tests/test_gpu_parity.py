@@ -1,0 +1,203 @@
+"""GPU parity: the gfx950 engine against the reference goldens and the CPU oracle.
+
+All comparisons are bit-exact (integer simulation): statuses, simulator time, final node
+tokens, snapshot completion ticks, snapshot token maps and per-channel recorded
+message sequences.  Full-size batches (BASELINE configs 2 and 3 per GPU) are checked
+through batch checksums against the oracle's own full-batch run plus sampled
+instance-by-instance comparisons.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from enginecheck import (batch_sums_from_oracle, canonical, cl, compare_instance, engine_run,
+                         oracle_batch, oracle_run)
+from snapcheck import TEST_DATA, assert_equal, check_tokens, read_snapshot_file, scenarios
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("sc", scenarios(), ids=lambda s: s["name"])
+def test_reference_goldens_and_neighbours(sc):
+    """Instance 0 uses the reference seed: it must reproduce the golden files exactly.
+    Instances 1..255 use seeds +1..+255 and must match the oracle bit for bit."""
+    n = 256
+    sim = engine_run(sc["top"], sc["events"], n)
+    status = sim.status()
+    assert status[0] == 0
+    actual = []
+    for sid in range(sim.num_snapshots):
+        s = sim.CollectSnapshot(sid, 0)
+        actual.append((s.id, s.tokenMap, [m.astuple() for m in s.messages]))
+    check_tokens(sim.node_tokens(0), actual)
+    expected = sorted((read_snapshot_file(f) for f in sc["snaps"]), key=lambda s: s[0])
+    assert len(expected) == len(actual)
+    for e, a in zip(expected, actual):
+        assert_equal(e, a)
+    assert sim.time()[0] == sc["ticks"]
+    times = sim.time()
+    for i in range(n):
+        compare_instance(sim, i, oracle_run(sc["top"], sc["events"], seed=O.REFERENCE_SEED + i),
+                         status=status, times=times)
+
+
+def test_counters_match_oracle():
+    sc = [s for s in scenarios() if s["name"] == "Test8NodesConcurrentSnapshots"][0]
+    n = 2048
+    sim = engine_run(sc["top"], sc["events"], n)
+    _, st, ticks, cnt, _ = oracle_batch(sc["top"], sc["events"], n)
+    got = sim.counters(only_ok=False)
+    assert got["push"] == cnt[:, 0].sum()
+    assert got["peek"] == cnt[:, 1].sum()
+    assert got["pop_tok"] == cnt[:, 2].sum()
+    assert got["pop_mk"] == cnt[:, 3].sum()
+    assert got["ticks"] == ticks.sum()
+    ok = st == 0
+    got_ok = sim.counters(only_ok=True)
+    assert got_ok["recorded"] == cnt[ok, 4].sum()
+    assert got_ok["completed"] == cnt[ok, 6].sum()
+
+
+def _checksums(sim):
+    return dict(zip(cl.SUM_NAMES, sim.checksums().tolist()))
+
+
+@pytest.mark.parametrize("cfg", [("10nodes.top", "10nodes.events", 65536),
+                                 ("8nodes.top", "8nodes-concurrent-snapshots.events", 131072)],
+                         ids=["C2_10nodes_x65536", "C3_8nodes_concurrent_x131072"])
+def test_full_batch_checksums(cfg):
+    """BASELINE configs at full per-GPU size: checksum of checksums vs the oracle's run
+    of every instance, plus conservation properties and sampled exact comparisons."""
+    top, events, n = cfg
+    sim = engine_run(top, events, n)
+    sums = _checksums(sim)
+    _, st, ticks, cnt, hashes = oracle_batch(top, events, n, threads=16)
+    want = batch_sums_from_oracle(st, cnt, hashes)
+    for k, v in want.items():
+        assert sums[k] == v, f"{k}: engine {sums[k]} vs oracle {v}"
+    assert sums["cut_residual"] == 0          # every snapshot is a consistent cut
+    assert sums["final_residual"] == 0        # checkTokens (test_common.go:298-328)
+    status = sim.status()
+    assert np.array_equal(status, st)
+    assert np.array_equal(sim.time()[st == 0], ticks[st == 0])
+    rng = np.random.default_rng(7)
+    sample = np.concatenate([[0, n - 1], rng.choice(n, 48, replace=False), np.nonzero(st != 0)[0][:16]])
+    times = sim.time()
+    for i in sample:
+        compare_instance(sim, int(i), oracle_run(top, events, seed=O.REFERENCE_SEED + int(i)),
+                         status=status, times=times)
+
+
+def test_fifo_spill_to_hbm():
+    """Two LDS slots per channel force deep channels through the HBM spill ring."""
+    top, events, n = "10nodes.top", "10nodes.events", 4096
+    sim = engine_run(top, events, n, fifo_lds_slots=2)
+    _, st, ticks, cnt, hashes = oracle_batch(top, events, n)
+    sums = _checksums(sim)
+    want = batch_sums_from_oracle(st, cnt, hashes)
+    for k, v in want.items():
+        assert sums[k] == v
+    for i in (0, 1, 17, 4095):
+        compare_instance(sim, i, oracle_run(top, events, seed=O.REFERENCE_SEED + i))
+
+
+def test_explicit_schedule_matches_oracle():
+    top, events, n = "8nodes.top", "8nodes-concurrent-snapshots.events", 512
+    rng = np.random.default_rng(3)
+    sched = rng.integers(0, 5, size=(n, 97), dtype=np.uint8)
+    sim = engine_run(top, events, n, schedule=sched)
+    status, times = sim.status(), sim.time()
+    for i in range(0, n, 7):
+        compare_instance(sim, i, oracle_run(top, events, schedule=sched[i]), status=status, times=times)
+
+
+def test_delay_exhausted():
+    top, events, n = "3nodes.top", "3nodes-simple.events", 64
+    sched = np.zeros((n, 4), dtype=np.uint8)  # 10 draws needed
+    sim = engine_run(top, events, n, schedule=sched)
+    assert (sim.status() == cl.INST_DELAY_EXHAUSTED).all()
+    ref = oracle_run(top, events, schedule=sched[0])
+    assert ref.status == O.DELAY_EXHAUSTED
+
+
+def test_incremental_flush_equals_one_shot():
+    """Flushing after every event (state saved/restored through HBM) == one launch."""
+    top = "8nodes.top"
+    lines = open(os.path.join(TEST_DATA, "8nodes-concurrent-snapshots.events")).read().split("\n")
+    n = 256
+    a = engine_run(top, "8nodes-concurrent-snapshots.events", n)
+    b = cl.ChandyLamportSim(n)
+    b.read_topology_file(os.path.join(TEST_DATA, top))
+    for line in lines:
+        if not line:
+            continue
+        f = line.split()
+        if f[0] == "send":
+            b.ProcessEvent(cl.PassTokenEvent(f[1], f[2], int(f[3])))
+        elif f[0] == "snapshot":
+            b.ProcessEvent(cl.SnapshotEvent(f[1]))
+        else:
+            b.Tick(int(f[1]) if len(f) > 1 else 1)
+        b.flush()
+    b.drain()
+    b.flush()
+    assert np.array_equal(a.status(), b.status())
+    assert np.array_equal(a.time(), b.time())
+    assert np.array_equal(a.checksums(), b.checksums())
+
+
+def test_hang_and_unknown_dest():
+    top = "3\nA 5\nB 5\nC 0\nA B\nB C\nC B\n"      # A has no in-links
+    sim = engine_run(top, "snapshot A\ntick 3\n", 64, max_drain_ticks=200)
+    assert (sim.status() == cl.INST_HANG).all()
+    ref = oracle_run(top, "snapshot A\ntick 3\n", seed=O.REFERENCE_SEED, max_drain=200)
+    assert ref.status == O.HANG
+    sim2 = engine_run(top, "send A B 1\nsend A C 1\ntick\n", 64)
+    assert (sim2.status() == cl.INST_FATAL_UNKNOWN_DEST).all()
+    sim3 = engine_run(top, "send C B 1\n", 64)
+    assert (sim3.status() == cl.INST_FATAL_INSUFFICIENT_TOKENS).all()
+
+
+def _random_scenario(rng, n_nodes, n_events):
+    ids = [f"N{k}" for k in range(1, n_nodes + 1)]   # lexicographic != numeric order (N10 < N2)
+    tokens = {i: int(rng.integers(0, 30)) for i in ids}
+    edges = set()
+    for k in range(n_nodes):                          # a ring keeps every node reachable
+        edges.add((ids[k], ids[(k + 1) % n_nodes]))
+    for _ in range(int(rng.integers(0, 3 * n_nodes))):
+        a, b = rng.choice(ids, 2, replace=False)
+        edges.add((str(a), str(b)))
+    top = f"{n_nodes}\n" + "".join(f"{i} {tokens[i]}\n" for i in ids) + "".join(f"{a} {b}\n" for a, b in sorted(edges))
+    ev = []
+    snaps = 0
+    out = {}
+    for a, b in edges:
+        out.setdefault(a, []).append(b)
+    for _ in range(n_events):
+        r = rng.random()
+        if r < 0.6:
+            a = str(rng.choice(ids))
+            b = str(rng.choice(out[a]))
+            ev.append(f"send {a} {b} {int(rng.integers(0, 4))}")
+        elif r < 0.75 and snaps < 12:
+            ev.append(f"snapshot {rng.choice(ids)}")
+            snaps += 1
+        else:
+            ev.append(f"tick {int(rng.integers(1, 4))}")
+    return top, "\n".join(ev) + "\n"
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_scenarios(seed):
+    """Random digraphs (up to 14 nodes, multi-source receivers, overlapping snapshots,
+    data-dependent fatals) against the oracle."""
+    rng = np.random.default_rng(100 + seed)
+    top, events = _random_scenario(rng, int(rng.integers(2, 15)), int(rng.integers(5, 60)))
+    n = 128
+    sim = engine_run(top, events, n, fifo_lds_slots=4)
+    status, times = sim.status(), sim.time()
+    for i in range(n):
+        compare_instance(sim, i, oracle_run(top, events, seed=O.REFERENCE_SEED + i),
+                         status=status, times=times)
