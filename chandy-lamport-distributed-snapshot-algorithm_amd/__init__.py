@@ -26,6 +26,8 @@ __all__ = ["ChandyLamportSim", "GlobalSnapshot", "MsgSnapshot", "PassTokenEvent"
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libclsnap.so")
+if os.environ.get("CLSNAP_VARIANT"):  # diagnostic ablation builds (Makefile `variant`)
+    LIB_PATH = os.path.join(HERE, "lib", f"libclsnap_{os.environ['CLSNAP_VARIANT']}.so")
 
 REFERENCE_SEED = 8053172852482175523 + 1  # snapshot_test.go:9,20 rand.Seed(seed + 1)
 MAX_DELAY = 5                              # sim.go:10

@@ -96,8 +96,9 @@ struct ExecParams {
   int32_t n_nodes, n_ch;
   Layout lay;
   int32_t n_started_before;  // snapshots started by ops before op_begin
-  // delays: sched[inst * draws + k] (kernel argument)
-  int64_t draws;
+  // delays: draw k of an instance is sched[inst * sched_row + k], k < draws
+  // (sched is a kernel argument; sched_row is a multiple of 16 for 16-byte windows)
+  int64_t draws, sched_row;
   int64_t n_inst, stride;
   int32_t fresh;
   // state / outputs (instance-fastest, [k][stride])

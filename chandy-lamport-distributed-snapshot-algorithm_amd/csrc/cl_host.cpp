@@ -237,7 +237,8 @@ struct cl_sim {
   int64_t seed_base = 8053172852482175524LL;  // snapshot_test.go:9,20 (seed + 1)
   std::vector<uint8_t> user_sched;
   int64_t user_draws = 0;
-  int64_t dev_draws = -1;  // row length of the schedule resident on the device
+  int64_t dev_draws = -1;  // valid draws per instance of the schedule resident on the device
+  int64_t dev_row = 0;     // its row stride (multiple of 16)
 
   // device
   bool dev_ready = false;
@@ -409,13 +410,19 @@ struct cl_sim {
       if (rc) return rc;
       HIP_TRY(hipMemcpy(d_sched.p, sched.data(), sched.size(), hipMemcpyHostToDevice));
       dev_draws = D;  // longer rows of the same streams: saved draw cursors stay valid
+      dev_row = D;
       return CL_OK;
     }
     if (dev_draws == user_draws) return CL_OK;
-    int rc = d_sched.ensure(user_sched.size());
+    const int64_t row = (user_draws + 15) / 16 * 16;
+    std::vector<uint8_t> padded((size_t)(row * n_inst), 0);
+    for (int64_t i = 0; i < n_inst; ++i)
+      std::memcpy(&padded[(size_t)(i * row)], &user_sched[(size_t)(i * user_draws)], (size_t)user_draws);
+    int rc = d_sched.ensure(padded.size());
     if (rc) return rc;
-    HIP_TRY(hipMemcpy(d_sched.p, user_sched.data(), user_sched.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_sched.p, padded.data(), padded.size(), hipMemcpyHostToDevice));
     dev_draws = user_draws;
+    dev_row = row;
     return CL_OK;
   }
 
@@ -468,6 +475,7 @@ struct cl_sim {
     p.lay = lay;
     p.n_started_before = n_started_before;
     p.draws = dev_draws;
+    p.sched_row = dev_row;
     p.n_inst = n_inst;
     p.stride = stride;
     p.fresh = op_begin == 0 ? 1 : 0;

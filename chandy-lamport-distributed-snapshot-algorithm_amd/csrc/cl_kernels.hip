@@ -21,6 +21,16 @@
 
 #include "cl_engine.h"
 
+// Diagnostic ablations (never set in the shipped build): CLSNAP_ABL_NOSTORE drops the
+// snapshot-output stores inside the tick loop, CLSNAP_ABL_NODELAYLOAD replaces the delay
+// schedule with zeros.  Outputs are wrong in those builds; only timing is meaningful.
+#ifndef CLSNAP_ABL_NOSTORE
+#define CLSNAP_ABL_NOSTORE 0
+#endif
+#ifndef CLSNAP_ABL_NODELAYLOAD
+#define CLSNAP_ABL_NODELAYLOAD 0
+#endif
+
 namespace clsnap {
 namespace {
 
@@ -37,7 +47,49 @@ struct Lane {
   int32_t time, dptr, status, ndone;
   uint32_t peek, pop_tok, pop_mk, push;
   bool alive;
+  // Delay window: draws [wbase, wbase+16) in d0..d3, the next 16 in n0..n3 (in flight).
+  int32_t wbase;
+  uint32_t d0, d1, d2, d3, n0, n1, n2, n3;
 };
+
+// Load the 16 draws starting at byte offset k of this instance's schedule row.
+__device__ __forceinline__ uint4 load_window(const Ctx& x, const Lane& ln, int32_t k) {
+  if (CLSNAP_ABL_NODELAYLOAD || k >= x.p.sched_row) return make_uint4(0, 0, 0, 0);
+  return *reinterpret_cast<const uint4*>(x.sched + ln.inst * x.p.sched_row + k);
+}
+
+__device__ __forceinline__ void open_window(const Ctx& x, Lane& ln) {
+  ln.wbase = ln.dptr & ~15;
+  const uint4 a = load_window(x, ln, ln.wbase);
+  const uint4 b = load_window(x, ln, ln.wbase + 16);
+  ln.d0 = a.x; ln.d1 = a.y; ln.d2 = a.z; ln.d3 = a.w;
+  ln.n0 = b.x; ln.n1 = b.y; ln.n2 = b.z; ln.n3 = b.w;
+  for (int32_t k = ln.wbase; k < ln.dptr; ++k) {  // resume mid-window
+    ln.d0 = __builtin_amdgcn_alignbit(ln.d1, ln.d0, 8);
+    ln.d1 = __builtin_amdgcn_alignbit(ln.d2, ln.d1, 8);
+    ln.d2 = __builtin_amdgcn_alignbit(ln.d3, ln.d2, 8);
+    ln.d3 >>= 8;
+  }
+}
+
+// Next delay draw (replaces rand.Intn(maxDelay), sim.go:101); caller checked dptr < draws.
+// The current window is consumed from its low byte and shifted down (v_alignbit), so no
+// runtime-indexed register selection is needed.
+__device__ __forceinline__ uint32_t next_delay(const Ctx& x, Lane& ln) {
+  const uint32_t d = ln.d0 & 0xffu;
+  ln.d0 = __builtin_amdgcn_alignbit(ln.d1, ln.d0, 8);
+  ln.d1 = __builtin_amdgcn_alignbit(ln.d2, ln.d1, 8);
+  ln.d2 = __builtin_amdgcn_alignbit(ln.d3, ln.d2, 8);
+  ln.d3 >>= 8;
+  ln.dptr++;
+  if ((ln.dptr & 15) == 0) {  // slide: the prefetched window becomes current, prefetch the next one
+    ln.wbase += 16;
+    ln.d0 = ln.n0; ln.d1 = ln.n1; ln.d2 = ln.n2; ln.d3 = ln.n3;
+    const uint4 b = load_window(x, ln, ln.wbase + 16);
+    ln.n0 = b.x; ln.n1 = b.y; ln.n2 = b.z; ln.n3 = b.w;
+  }
+  return d;
+}
 
 #define LW(k) (ln.L[(uint32_t)(k) << 6])
 
@@ -55,8 +107,7 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t c, uint32_t
   const uint32_t cnt = (chw >> 8) & 0xffu;
   if (cnt >= (uint32_t)kMaxQueued) { fail(ln, ST_FIFO_OVERFLOW); return; }
   if (ln.dptr >= p.draws) { fail(ln, ST_DELAY_EXHAUSTED); return; }
-  const uint32_t delay = x.sched[ln.inst * p.draws + ln.dptr];
-  ln.dptr++;
+  const uint32_t delay = next_delay(x, ln);
   const uint32_t e = payload | ((uint32_t)(ln.time + 1 + (int32_t)delay) << 16);
   const uint32_t cap = 1u << lay.cap_log2;
   if (cnt < cap) {
@@ -86,12 +137,14 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, int32_t w, 
                                              int32_t arrive) {
   const ExecParams& p = x.p;
   const Layout& lay = p.lay;
-  p.snap_tok[((int64_t)sid * p.n_nodes + w) * p.stride + ln.inst] = (int32_t)LW(lay.w_tok + w);
+  if (!CLSNAP_ABL_NOSTORE)
+    p.snap_tok[((int64_t)sid * p.n_nodes + w) * p.stride + ln.inst] = (int32_t)LW(lay.w_tok + w);
   const int32_t k0 = x.t.in_off[w], k1 = x.t.in_off[w + 1];
   for (int32_t k = k0; k < k1; ++k) {
     const int32_t cc = x.t.in_ch[k];
     const uint32_t td = LW(lay.w_chw + cc) >> 16;
-    p.snap_rec[((int64_t)sid * p.n_ch + cc) * p.stride + ln.inst] = cc == arrive ? (td | (td << 16)) : td;
+    if (!CLSNAP_ABL_NOSTORE)
+      p.snap_rec[((int64_t)sid * p.n_ch + cc) * p.stride + ln.inst] = cc == arrive ? (td | (td << 16)) : td;
   }
 }
 
@@ -104,7 +157,7 @@ __device__ __forceinline__ void node_complete(const ExecParams& p, Lane& ln, int
   const uint32_t n = ((dw >> sh) & 0xffu) + 1;
   LW(di) = (dw & ~(0xffu << sh)) | (n << sh);
   if (n == (uint32_t)p.n_nodes) {
-    p.snap_tick[(int64_t)sid * p.stride + ln.inst] = ln.time;
+    if (!CLSNAP_ABL_NOSTORE) p.snap_tick[(int64_t)sid * p.stride + ln.inst] = ln.time;
     ln.ndone++;
   }
 }
@@ -126,8 +179,9 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, int32_t w,
     broadcast_marker(x, ln, w, sid);
   } else {
     const uint32_t td = LW(lay.w_chw + c) >> 16;
-    reinterpret_cast<uint16_t*>(p.snap_rec)[2 * (((int64_t)sid * p.n_ch + c) * p.stride + ln.inst) + 1] =
-        (uint16_t)td;
+    if (!CLSNAP_ABL_NOSTORE)
+      reinterpret_cast<uint16_t*>(p.snap_rec)[2 * (((int64_t)sid * p.n_ch + c) * p.stride + ln.inst) + 1] =
+          (uint16_t)td;
     pend = (int32_t)((pw >> sh) & 0xffu) - 1;
   }
   LW(pi) = (pw & ~(0xffu << sh)) | ((uint32_t)pend << sh);
@@ -209,6 +263,7 @@ __global__ __launch_bounds__(64) void cl_exec_kernel(ExecParams p, const int32_t
     ln.push = (uint32_t)r[R_PUSH * p.stride];
   }
   ln.alive = valid && ln.status == ST_OK;
+  if (ln.alive) open_window(x, ln);
   int32_t n_started = p.n_started_before;
 
   for (int32_t i = p.op_begin; i < p.op_end; ++i) {
