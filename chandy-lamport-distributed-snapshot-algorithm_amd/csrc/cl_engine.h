@@ -8,8 +8,8 @@ namespace clsnap {
 // ---- event program ("op tape") ---------------------------------------------
 // Every instance executes the same program; ops are read with scalar loads.
 enum OpKind : int32_t {
-  OP_SEND = 1,   // a = src rank, b = channel (-1: unknown dest), c = tokens  (node.go:112-131)
-  OP_SNAP = 2,   // a = node rank, b = snapshot id                          (sim.go:105-123)
+  OP_SEND = 1,   // a = src rank, b = out-index at src (-1: unknown dest), c = tokens  (node.go:112-131)
+  OP_SNAP = 2,   // a = node rank, b = snapshot id, c = outdeg(a)                   (sim.go:105-123)
   OP_TICK = 3,   // a = number of ticks                                      (sim.go:71-95)
   OP_DRAIN = 4,  // a = max drain ticks, b = extra ticks (maxDelay+1)        (test_common.go:123-137)
 };
@@ -44,13 +44,19 @@ constexpr uint32_t kTokDelivOne = 1u << 16;
 constexpr int32_t kMaxQueued = 255;
 constexpr int32_t kMaxChannelTokens = 65535;
 
-// ---- limits of the small-graph (instance-per-lane) kernel -----------------
-constexpr int32_t kMaxSnapshots = 32;   // STARTED bitmask per node
-constexpr int32_t kMaxNodes = 255;      // u8 completion counters
+// ---- limits of the node-parallel kernel -----------------------------------
+constexpr int32_t kMaxSnapshots = 32;   // per-node STARTED bitmask
+constexpr int32_t kMaxNodes = 64;       // one instance = one segment of a 64-lane wave
+constexpr int32_t kMaxDegree = 127;     // 7-bit out-index in a pick word
 constexpr int32_t kWave = 64;
+constexpr int32_t kWavesPerBlock = 4;
 constexpr int32_t kMaxLdsBytes = 160 * 1024;
 
-// Register image saved per instance between launches (regs[r * stride + inst]).
+// Pick word published by a sender lane each tick (phase A):
+//   bit 31 marker, bit 30 valid, bits 22..16 out-index, bits 15..0 payload.
+constexpr uint32_t kPickValid = 0x40000000u;
+
+// Per-instance results written at the end of every launch (regs[r * stride + inst]).
 enum : int32_t {
   R_TIME = 0,
   R_DRAW = 1,
@@ -64,29 +70,57 @@ enum : int32_t {
   R_NUM = 9,
 };
 
-// LDS image of one instance, in 32-bit words.  Word k of the lane's instance lives at
-// lds[k * 64 + lane]: every lane owns one bank column, so any per-lane index is
-// conflict-free (bank = lane mod 32 for ds_read/write_b32).
-struct Layout {
-  int32_t cap_log2;   // LDS ring slots per channel = 1 << cap_log2
-  int32_t ocap_log2;  // HBM spill ring per channel = 1 << ocap_log2 (-1 = none)
-  int32_t sp;         // words of u8 pending counters per node = ceil(S_cap / 4)
-  int32_t w_fifo, w_chw, w_tok, w_started, w_pend, w_done, words;
+// Per-lane registers kept in the state image between launches.
+enum : int32_t {
+  G_TOKENS = 0, G_STARTED, G_TIME, G_DRAW, G_STATUS, G_PEEK, G_POP_TOK, G_POP_MK, G_PUSH, G_NUM
 };
 
-inline Layout make_layout(int32_t n_nodes, int32_t n_ch, int32_t cap_log2, int32_t ocap_log2,
+// LDS of one wave: a private column per lane (word k of lane l at lds[k * 64 + l]; a
+// lane only indexes its own column, so every data-dependent access is conflict-free)
+// followed by a small region shared by the wave's lanes.
+struct Layout {
+  int32_t cap_log2;   // LDS ring slots per out-channel = 1 << cap_log2
+  int32_t ocap_log2;  // HBM spill ring per channel = 1 << ocap_log2 (-1 = none)
+  int32_t od, id;     // max out-degree / in-degree over nodes
+  int32_t s_cap;      // snapshot ids provisioned
+  int32_t sp;         // u8 pending counters per node: words = ceil(s_cap / 4)
+  int32_t ipw;        // instances per wave = 64 / N
+  // private column (words)
+  int32_t w_fifo, w_chw, w_cur, w_int, w_pend, w_trig, priv;
+  // shared region (words, after the 64 private columns)
+  int32_t x_pick, x_tslot, x_off, x_done, x_ndone, x_acc, shared;
+  int32_t wave_words;
+  // state image per instance (words): per node priv + G_NUM, then s_cap done counters + ndone
+  int32_t state_words;
+};
+
+inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_log2, int32_t ocap_log2,
                           int32_t s_cap) {
   Layout L;
   L.cap_log2 = cap_log2;
   L.ocap_log2 = ocap_log2;
+  L.od = od;
+  L.id = id;
+  L.s_cap = s_cap;
   L.sp = (s_cap + 3) / 4;
+  L.ipw = n_nodes > 0 ? kWave / n_nodes : 0;
   L.w_fifo = 0;
-  L.w_chw = n_ch << cap_log2;
-  L.w_tok = L.w_chw + n_ch;
-  L.w_started = L.w_tok + n_nodes;
-  L.w_pend = L.w_started + n_nodes;
-  L.w_done = L.w_pend + n_nodes * L.sp;
-  L.words = L.w_done + L.sp;
+  L.w_chw = od << cap_log2;
+  L.w_cur = L.w_chw + od;
+  L.w_int = L.w_cur + id;
+  L.w_pend = L.w_int + id;
+  L.w_trig = L.w_pend + L.sp;
+  L.priv = L.w_trig + id;
+  const int32_t base = L.priv * kWave;
+  L.x_pick = base;
+  L.x_tslot = base + kWave;
+  L.x_off = base + 2 * kWave;
+  L.x_done = base + 3 * kWave;
+  L.x_ndone = L.x_done + L.ipw * s_cap;
+  L.x_acc = L.x_ndone + L.ipw;
+  L.shared = L.x_acc + 5 * L.ipw - base;
+  L.wave_words = (base + L.shared + 3) / 4 * 4;
+  L.state_words = n_nodes * (L.priv + G_NUM) + s_cap + 1;
   return L;
 }
 
@@ -97,13 +131,13 @@ struct ExecParams {
   Layout lay;
   int32_t n_started_before;  // snapshots started by ops before op_begin
   // delays: draw k of an instance is sched[inst * sched_row + k], k < draws
-  // (sched is a kernel argument; sched_row is a multiple of 16 for 16-byte windows)
   int64_t draws, sched_row;
   int64_t n_inst, stride;
   int32_t fresh;
   // state / outputs (instance-fastest, [k][stride])
-  uint32_t* state;
-  int32_t* regs;
+  uint32_t* state;     // [state_words]
+  int32_t* regs;       // [R_NUM]
+  int32_t* fin_tok;    // [N] final node tokens
   int32_t* snap_tok;   // [S_cap][N]
   uint32_t* snap_rec;  // [S_cap][C]  lo16 = begin, hi16 = end (channel token cursor)
   int32_t* snap_tick;  // [S_cap]
@@ -115,34 +149,22 @@ struct SumParams {
   int32_t n_nodes, n_ch, s_cap, n_sids;
   int64_t n_inst, stride;
   const int32_t* regs;
+  const int32_t* fin_tok;
   const int32_t* snap_tok;
   const uint32_t* snap_rec;
   const int32_t* snap_tick;
-  const uint32_t* state;
-  Layout lay;
   const int32_t* hist_off;  // [C+1] token history of each channel (shared by all instances)
   const int32_t* hist_val;
   int64_t total_tokens;
   unsigned long long* out;  // [CL_NUM_SUMS]
 };
 
-// Topology image (one int32 array, uniform across lanes, passed as a __restrict__
-// kernel argument so the kernel reads it through the scalar cache):
-//   [0, N]            out_off  channels of sender v are out_off[v] .. out_off[v+1]-1 (dest order)
-//   [N+1, N+1+C)      ch_dst   dest rank of channel c
-//   next N+1          in_off
-//   next C            in_ch    channels into node w, ordered by src rank
-//   next N            init_tok
-struct TopoView {
-  const int32_t* out_off;
-  const int32_t* ch_dst;
-  const int32_t* in_off;
-  const int32_t* in_ch;
-  const int32_t* init_tok;
-};
-
+// Topology image (uint32, uniform per node, read once per lane at kernel start):
+//   node v block at v * (3 + id): [indeg, outdeg, out_off, in[0..id)]
+//     in[k] = src rank (bits 7..0) | sender's out-index of this channel (15..8) | channel id (31..16)
+//   then init_tok[N] at N * (3 + id)
 // Launchers (cl_kernels.hip); return hipError_t as int.
-int launch_exec(const ExecParams& p, const int32_t* topo, const Op* ops, const uint8_t* sched, void* stream);
+int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream);
 int launch_checksums(const SumParams& p, void* stream);
 
 // Snapshot content hash (shared definition with oracle/cl_oracle.c orc_snapshot_hash).

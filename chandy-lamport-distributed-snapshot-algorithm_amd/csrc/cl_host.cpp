@@ -217,6 +217,7 @@ struct cl_sim {
   std::vector<int> rank_of;    // insertion index -> rank
   std::vector<int> by_rank;    // rank -> insertion index
   std::vector<int32_t> out_off, ch_dst, ch_src, in_off, in_ch, init_tok;
+  int32_t max_out = 0, max_in = 0;
   int64_t total_tokens = 0;
 
   // event program
@@ -270,7 +271,8 @@ struct cl_sim {
   bool need_fresh = true;
   DevBuf<Op> d_ops;
   size_t ops_uploaded = 0;
-  DevBuf<int32_t> d_topo;
+  DevBuf<uint32_t> d_topo;
+  DevBuf<int32_t> d_fin_tok;
   DevBuf<uint8_t> d_sched;
   DevBuf<uint32_t> d_state;
   DevBuf<int32_t> d_regs;
@@ -292,7 +294,7 @@ struct cl_sim {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
-      d_snap_tok.release(); d_snap_rec.release(); d_snap_tick.release(); d_ovf.release();
+      d_snap_tok.release(); d_snap_rec.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
       d_ovh.release(); d_hist.release(); d_sums.release();
       for (auto& e : ev_pool) {
         (void)hipEventDestroy(e.first);
@@ -311,7 +313,7 @@ struct cl_sim {
   int freeze() {
     if (frozen) return CL_OK;
     const int n = (int)ids.size();
-    if (n > kMaxNodes) return set_err(CL_E_LIMIT, "%d nodes exceed the small-graph engine limit %d", n, kMaxNodes);
+    if (n > kMaxNodes) return set_err(CL_E_LIMIT, "%d nodes exceed the node-parallel engine limit %d", n, kMaxNodes);
     by_rank.resize(n);
     for (int i = 0; i < n; ++i) by_rank[i] = i;
     std::sort(by_rank.begin(), by_rank.end(), [&](int a, int b) { return ids[a] < ids[b]; });
@@ -344,6 +346,12 @@ struct cl_sim {
       init_tok[r] = (int32_t)init_tokens[by_rank[r]];
       total_tokens += init_tokens[by_rank[r]];
     }
+    max_out = max_in = 0;
+    for (int v = 0; v < n; ++v) {
+      max_out = std::max(max_out, out_off[v + 1] - out_off[v]);
+      max_in = std::max(max_in, in_off[v + 1] - in_off[v]);
+    }
+    if (max_out > kMaxDegree) return set_err(CL_E_LIMIT, "out-degree %d exceeds %d", max_out, kMaxDegree);
     hist.assign(C, {});
     depth_bound.assign(C, 0);
     frozen = true;
@@ -385,17 +393,23 @@ struct cl_sim {
   }
 
   int upload_topology() {
-    const int n = (int)ids.size(), C = (int)ch_dst.size();
-    std::vector<int32_t> t;
-    t.insert(t.end(), out_off.begin(), out_off.end());
-    t.insert(t.end(), ch_dst.begin(), ch_dst.end());
-    t.insert(t.end(), in_off.begin(), in_off.end());
-    t.insert(t.end(), in_ch.begin(), in_ch.end());
-    t.insert(t.end(), init_tok.begin(), init_tok.end());
-    (void)n; (void)C;
+    const int n = (int)ids.size();
+    const int W = 3 + max_in;
+    std::vector<uint32_t> t((size_t)n * W + n, 0u);
+    for (int v = 0; v < n; ++v) {
+      uint32_t* b = &t[(size_t)v * W];
+      b[0] = (uint32_t)(in_off[v + 1] - in_off[v]);
+      b[1] = (uint32_t)(out_off[v + 1] - out_off[v]);
+      b[2] = (uint32_t)out_off[v];
+      for (int k = in_off[v]; k < in_off[v + 1]; ++k) {
+        const int c = in_ch[k], src = ch_src[c];
+        b[3 + (k - in_off[v])] = (uint32_t)src | ((uint32_t)(c - out_off[src]) << 8) | ((uint32_t)c << 16);
+      }
+      t[(size_t)n * W + v] = (uint32_t)init_tok[v];
+    }
     int rc = d_topo.ensure(t.size());
     if (rc) return rc;
-    HIP_TRY(hipMemcpy(d_topo.p, t.data(), t.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_topo.p, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     return CL_OK;
   }
 
@@ -431,16 +445,19 @@ struct cl_sim {
     const int n = (int)ids.size(), C = (int)ch_dst.size();
     int32_t want_s = std::max<int32_t>(4, (n_sids + 3) / 4 * 4);
     int ocap = ocap_log2_needed();
-    if (!need_fresh && want_s <= s_cap && ocap <= lay.ocap_log2 && lay.cap_log2 == cap_log2) return CL_OK;
+    if (!need_fresh && lay.wave_words && want_s <= s_cap && ocap <= lay.ocap_log2 && lay.cap_log2 == cap_log2)
+      return CL_OK;
     s_cap = std::max(want_s, s_cap);
     if (s_cap > kMaxSnapshots) return set_err(CL_E_LIMIT, "more than %d snapshots", kMaxSnapshots);
-    Layout L = make_layout(n, C, cap_log2, std::max(ocap, lay.words ? lay.ocap_log2 : -1), s_cap);
-    if ((int64_t)L.words * kWave * 4 > kMaxLdsBytes)
-      return set_err(CL_E_LIMIT, "instance state of %d words exceeds LDS (lower fifo slots or graph size)", L.words);
+    if (n == 0) return set_err(CL_E_STATE, "the topology has no nodes");
+    Layout L = make_layout(n, max_out, max_in, cap_log2, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), s_cap);
+    if ((int64_t)L.wave_words * kWavesPerBlock * 4 > kMaxLdsBytes)
+      return set_err(CL_E_LIMIT, "per-wave state of %d words exceeds LDS (lower fifo slots or degree)", L.wave_words);
     lay = L;
     int rc;
-    if ((rc = d_state.ensure((size_t)lay.words * stride))) return rc;
+    if ((rc = d_state.ensure((size_t)lay.state_words * stride))) return rc;
     if ((rc = d_regs.ensure((size_t)R_NUM * stride))) return rc;
+    if ((rc = d_fin_tok.ensure((size_t)n * stride))) return rc;
     if ((rc = d_snap_tok.ensure((size_t)s_cap * n * stride))) return rc;
     if ((rc = d_snap_rec.ensure((size_t)s_cap * std::max(C, 1) * stride))) return rc;
     if ((rc = d_snap_tick.ensure((size_t)s_cap * stride))) return rc;
@@ -481,6 +498,7 @@ struct cl_sim {
     p.fresh = op_begin == 0 ? 1 : 0;
     p.state = d_state.p;
     p.regs = d_regs.p;
+    p.fin_tok = d_fin_tok.p;
     p.snap_tok = d_snap_tok.p;
     p.snap_rec = d_snap_rec.p;
     p.snap_tick = d_snap_tick.p;
@@ -564,8 +582,7 @@ struct cl_sim {
     HIP_TRY(hipMemcpy(h_snap_tok.data(), d_snap_tok.p, h_snap_tok.size() * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(h_snap_rec.data(), d_snap_rec.p, h_snap_rec.size() * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(h_snap_tick.data(), d_snap_tick.p, h_snap_tick.size() * 4, hipMemcpyDeviceToHost));
-    if (n) HIP_TRY(hipMemcpy(h_tok.data(), d_state.p + (size_t)lay.w_tok * stride, h_tok.size() * 4,
-                             hipMemcpyDeviceToHost));
+    if (n) HIP_TRY(hipMemcpy(h_tok.data(), d_fin_tok.p, h_tok.size() * 4, hipMemcpyDeviceToHost));
     h_valid = true;
     return CL_OK;
   }
@@ -729,6 +746,7 @@ int cl_send_tokens(cl_sim* sim, const char* src, const char* dest, int64_t n) {
   const int b = sim->node_of(dest);
   const int ra = sim->rank_of[a];
   const int c = b < 0 ? -1 : sim->channel_of(ra, sim->rank_of[b]);
+  const int ko = c < 0 ? -1 : c - sim->out_off[ra];  // out-index of the link at its sender
   if (c >= 0) {
     if ((int64_t)sim->hist[c].size() >= kMaxChannelTokens)
       return set_err(CL_E_LIMIT, "more than %d token messages on one channel", kMaxChannelTokens);
@@ -736,7 +754,7 @@ int cl_send_tokens(cl_sim* sim, const char* src, const char* dest, int64_t n) {
     sim->depth_bound[c]++;
   }
   sim->sends++;
-  return sim->append(Op{OP_SEND, ra, c, (int32_t)n});
+  return sim->append(Op{OP_SEND, ra, ko, (int32_t)n});
 }
 
 int cl_start_snapshot(cl_sim* sim, const char* node, int32_t* out_sid) {
@@ -749,7 +767,8 @@ int cl_start_snapshot(cl_sim* sim, const char* node, int32_t* out_sid) {
   const int32_t sid = sim->n_sids++;
   for (auto& d : sim->depth_bound) d++;
   if (out_sid) *out_sid = sid;
-  return sim->append(Op{OP_SNAP, sim->rank_of[a], sid, 0});
+  const int r = sim->rank_of[a];
+  return sim->append(Op{OP_SNAP, r, sid, sim->out_off[r + 1] - sim->out_off[r]});
 }
 
 int cl_tick(cl_sim* sim, int32_t n) {
@@ -915,7 +934,7 @@ int cl_device_bytes(const cl_sim* sim, int64_t* bytes) {
   int64_t b = 0;
   b += sim->d_ops.n * sizeof(Op) + sim->d_topo.n * 4 + sim->d_sched.n + sim->d_state.n * 4 + sim->d_regs.n * 4;
   b += sim->d_snap_tok.n * 4 + sim->d_snap_rec.n * 4 + sim->d_snap_tick.n * 4 + sim->d_ovf.n * 4;
-  b += sim->d_ovh.n * 4 + sim->d_hist.n * 4 + sim->d_sums.n * 8;
+  b += sim->d_ovh.n * 4 + sim->d_hist.n * 4 + sim->d_sums.n * 8 + sim->d_fin_tok.n * 4;
   *bytes = b;
   return CL_OK;
 }
@@ -1030,8 +1049,7 @@ int cl_get_checksums(cl_sim* sim, int64_t* out) {
   p.snap_tok = sim->d_snap_tok.p;
   p.snap_rec = sim->d_snap_rec.p;
   p.snap_tick = sim->d_snap_tick.p;
-  p.state = sim->d_state.p;
-  p.lay = sim->lay;
+  p.fin_tok = sim->d_fin_tok.p;
   p.hist_off = sim->d_hist.p;
   p.hist_val = sim->d_hist.p + sim->hist.size() + 1;
   p.total_tokens = sim->total_tokens;

@@ -1,355 +1,428 @@
 // cl_kernels.hip -- gfx950 kernels of the Chandy-Lamport batch engine.
 //
-// cl_exec_kernel runs the event program (send / snapshot / tick / drain) for 64
-// independent simulator instances per wave, one instance per lane.  Each instance's
-// mutable state (channel FIFOs, node tokens, per-snapshot bookkeeping) lives in LDS for
-// the whole launch, laid out lane-column-major (word k of lane l at lds[k*64 + l]) so
-// every data-dependent per-lane access is bank-conflict free.  The topology and the
-// program are uniform across lanes and are read through the scalar cache.  Only the
-// delay schedule (1 B per draw), the snapshot outputs and the saved state touch HBM.
+// cl_exec_kernel runs the event program (send / snapshot / tick / drain) for a batch of
+// independent simulator instances.  Node-parallel layout: an instance of N nodes is a
+// segment of N consecutive lanes of a 64-lane wave (lane = node rank), 64/N instances
+// per wave, 4 independent waves per workgroup.  A node's mutable state lives in its
+// lane: tokens and the STARTED mask in VGPRs; its out-channel FIFOs (sender side), its
+// in-channel recording cursors (receiver side) and its per-snapshot pending counters in
+// the lane's private LDS column (word k at lds[k*64 + lane]: conflict-free for any
+// per-lane index).  Lanes exchange only three things per tick, through a small shared
+// LDS region: the packet each sender picked, the marker-broadcast draw counts, and their
+// exclusive prefix sums.  HBM carries the delay schedule (1 B per draw) and the snapshot
+// outputs.
 //
-// Semantics restated (paths relative to /root/reference/chandy_lamport):
-//   tick()          sim.go:71-95   senders in rank order, out-links in dest order,
-//                                  head-of-line only, at most one delivery per sender
-//   push()          node.go:107,126-130 + sim.go:100-102 (receiveTime = time+1+delay)
-//   handle_marker() node.go:149-171, CreateLocalSnapshot node.go:58-84
-//   token delivery  node.go:174-185 (recording kept as per-channel cursors)
-//   OP_SEND         node.go:112-131 (fatal checks in the reference's order)
-//   OP_SNAP         sim.go:105-123, node.go:198-212
-//   OP_DRAIN        test_common.go:123-137
+// One tick (sim.go:71-95) in four wave-synchronous phases:
+//   A pick     every sender scans its out-links in dest order and pops the first due head
+//              (head-of-line; <= 1 delivery per sender).  Pushes made later in the same
+//              tick can never be due in it, so picks from tick-start state are exact.
+//   B receive  every receiver handles the picks addressed to it in ascending sender rank,
+//              i.e. in the reference's delivery order: token -> tokens += n, cursor++;
+//              marker -> CreateLocalSnapshot / close channel / completion (node.go:149-185).
+//   C scan     first-receipt markers broadcast (node.go:97-109); the reference draws their
+//              delays in sender order, so draw offsets are the exclusive prefix sum of
+//              outdeg(receiver) over triggering senders (segmented wave scan).
+//   D push     receivers push markers on their out-links with delays from those offsets.
+// Reference map (paths relative to /root/reference/chandy_lamport): Tick sim.go:71-95,
+// GetReceiveTime sim.go:100-102, StartSnapshot sim.go:105-123, NotifyCompletedSnapshot
+// sim.go:126-131, CreateLocalSnapshot node.go:58-84, SendToNeighbors node.go:97-109,
+// SendTokens node.go:112-131, HandleMarker node.go:149-171, HandleToken node.go:174-185,
+// drain test_common.go:123-137.
 #include <hip/hip_runtime.h>
 
 #include "cl_engine.h"
 
-// Diagnostic ablations (never set in the shipped build): CLSNAP_ABL_NOSTORE drops the
-// snapshot-output stores inside the tick loop, CLSNAP_ABL_NODELAYLOAD replaces the delay
-// schedule with zeros.  Outputs are wrong in those builds; only timing is meaningful.
-#ifndef CLSNAP_ABL_NOSTORE
-#define CLSNAP_ABL_NOSTORE 0
-#endif
-#ifndef CLSNAP_ABL_NODELAYLOAD
-#define CLSNAP_ABL_NODELAYLOAD 0
-#endif
-
 namespace clsnap {
 namespace {
 
-// Uniform inputs: parameters, topology and delay schedule.
 struct Ctx {
   const ExecParams& p;
-  TopoView t;
-  const uint8_t* __restrict__ sched;
+  const Layout& lay;
+  uint32_t* P;  // this lane's private column: word k at P[k * 64]
+  uint32_t* X;  // this wave's LDS base (shared region at lay.x_*)
+  const uint8_t* __restrict__ row;  // this instance's delay row
+  int32_t lane, seg_base, v, seg;
+  int64_t inst;
+  uint64_t seg_mask;  // the instance's lanes
+  int32_t indeg, outdeg, out_off;
 };
 
 struct Lane {
-  uint32_t* L;  // lds + lane
-  int64_t inst;
-  int32_t time, dptr, status, ndone;
+  int32_t tokens;
+  uint32_t started;
+  int32_t time, draw, status;
   uint32_t peek, pop_tok, pop_mk, push;
-  bool alive;
-  // Delay window: draws [wbase, wbase+16) in d0..d3, the next 16 in n0..n3 (in flight).
-  int32_t wbase;
-  uint32_t d0, d1, d2, d3, n0, n1, n2, n3;
+  bool alive;    // instance still running (uniform within the segment)
+  int32_t flag;  // lane-local engine failure raised during an op/tick
 };
 
-// Load the 16 draws starting at byte offset k of this instance's schedule row.
-__device__ __forceinline__ uint4 load_window(const Ctx& x, const Lane& ln, int32_t k) {
-  if (CLSNAP_ABL_NODELAYLOAD || k >= x.p.sched_row) return make_uint4(0, 0, 0, 0);
-  return *reinterpret_cast<const uint4*>(x.sched + ln.inst * x.p.sched_row + k);
+#define PW(k) (x.P[(uint32_t)(k) << 6])
+#define XW(k) (x.X[(uint32_t)(k)])
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void open_window(const Ctx& x, Lane& ln) {
-  ln.wbase = ln.dptr & ~15;
-  const uint4 a = load_window(x, ln, ln.wbase);
-  const uint4 b = load_window(x, ln, ln.wbase + 16);
-  ln.d0 = a.x; ln.d1 = a.y; ln.d2 = a.z; ln.d3 = a.w;
-  ln.n0 = b.x; ln.n1 = b.y; ln.n2 = b.z; ln.n3 = b.w;
-  for (int32_t k = ln.wbase; k < ln.dptr; ++k) {  // resume mid-window
-    ln.d0 = __builtin_amdgcn_alignbit(ln.d1, ln.d0, 8);
-    ln.d1 = __builtin_amdgcn_alignbit(ln.d2, ln.d1, 8);
-    ln.d2 = __builtin_amdgcn_alignbit(ln.d3, ln.d2, 8);
-    ln.d3 >>= 8;
-  }
-}
-
-// Next delay draw (replaces rand.Intn(maxDelay), sim.go:101); caller checked dptr < draws.
-// The current window is consumed from its low byte and shifted down (v_alignbit), so no
-// runtime-indexed register selection is needed.
-__device__ __forceinline__ uint32_t next_delay(const Ctx& x, Lane& ln) {
-  const uint32_t d = ln.d0 & 0xffu;
-  ln.d0 = __builtin_amdgcn_alignbit(ln.d1, ln.d0, 8);
-  ln.d1 = __builtin_amdgcn_alignbit(ln.d2, ln.d1, 8);
-  ln.d2 = __builtin_amdgcn_alignbit(ln.d3, ln.d2, 8);
-  ln.d3 >>= 8;
-  ln.dptr++;
-  if ((ln.dptr & 15) == 0) {  // slide: the prefetched window becomes current, prefetch the next one
-    ln.wbase += 16;
-    ln.d0 = ln.n0; ln.d1 = ln.n1; ln.d2 = ln.n2; ln.d3 = ln.n3;
-    const uint4 b = load_window(x, ln, ln.wbase + 16);
-    ln.n0 = b.x; ln.n1 = b.y; ln.n2 = b.z; ln.n3 = b.w;
-  }
-  return d;
-}
-
-#define LW(k) (ln.L[(uint32_t)(k) << 6])
-
-__device__ __forceinline__ void fail(Lane& ln, int32_t st) {
-  ln.status = st;
-  ln.alive = false;
-}
-
-// Queue.Push (queue.go:18-20) with the receive time drawn at push (sim.go:100-102).
-__device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t c, uint32_t payload) {
-  if (!ln.alive) return;
-  const ExecParams& p = x.p;
-  const Layout& lay = p.lay;
-  const uint32_t chw = LW(lay.w_chw + c);
+// Queue.Push (queue.go:18-20) on out-link ko; receiveTime = time + 1 + draw (sim.go:101).
+// `k` is the index of the draw in this instance's delay stream.
+__device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int64_t k) {
+  const Layout& lay = x.lay;
+  if (k >= x.p.draws) { ln.flag = ST_DELAY_EXHAUSTED; return; }
+  const uint32_t chw = PW(lay.w_chw + ko);
   const uint32_t cnt = (chw >> 8) & 0xffu;
-  if (cnt >= (uint32_t)kMaxQueued) { fail(ln, ST_FIFO_OVERFLOW); return; }
-  if (ln.dptr >= p.draws) { fail(ln, ST_DELAY_EXHAUSTED); return; }
-  const uint32_t delay = next_delay(x, ln);
+  if (cnt >= (uint32_t)kMaxQueued) { ln.flag = ST_FIFO_OVERFLOW; return; }
+  const uint32_t delay = x.row[k];
   const uint32_t e = payload | ((uint32_t)(ln.time + 1 + (int32_t)delay) << 16);
   const uint32_t cap = 1u << lay.cap_log2;
   if (cnt < cap) {
-    LW(lay.w_fifo + ((uint32_t)c << lay.cap_log2) + ((chw + cnt) & (cap - 1))) = e;
-  } else {
-    // LDS ring full: the channel's younger packets spill to an HBM ring.
-    if (lay.ocap_log2 < 0 || cnt - cap >= (1u << lay.ocap_log2)) { fail(ln, ST_FIFO_OVERFLOW); return; }
+    PW(lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + ((chw + cnt) & (cap - 1))) = e;
+  } else {  // LDS ring full: younger packets of this channel spill to an HBM ring
+    if (lay.ocap_log2 < 0 || cnt - cap >= (1u << lay.ocap_log2)) { ln.flag = ST_FIFO_OVERFLOW; return; }
+    const int64_t c = x.out_off + ko;
     const uint32_t om = (1u << lay.ocap_log2) - 1;
-    const uint32_t h = p.ovh[(int64_t)c * p.stride + ln.inst];
-    p.ovf[(((int64_t)c << lay.ocap_log2) + ((h + cnt - cap) & om)) * p.stride + ln.inst] = e;
+    const uint32_t h = x.p.ovh[c * x.p.stride + x.inst];
+    x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.p.stride + x.inst] = e;
   }
-  LW(lay.w_chw + c) = chw + kCountOne;
+  PW(lay.w_chw + ko) = chw + kCountOne;
   ln.push++;
 }
 
-// SendToNeighbors (node.go:97-109): one draw per out-link, dest order.
-__device__ __forceinline__ void broadcast_marker(const Ctx& x, Lane& ln, int32_t w, int32_t sid) {
-  const int32_t e0 = x.t.out_off[w], e1 = x.t.out_off[w + 1];
-  for (int32_t c = e0; c < e1; ++c) push(x, ln, c, kMarkerBit | (uint32_t)sid);
-}
-
-// CreateLocalSnapshot (node.go:58-84): record tokens, open every in-channel except the
-// one the first marker arrived on (arrive = -1 for the initiator).  A channel's
-// recording is the half-open cursor interval [begin, end) over the tokens delivered on
-// it; end is written when the channel's marker arrives.
-__device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, int32_t w, int32_t sid,
-                                             int32_t arrive) {
+// CreateLocalSnapshot (node.go:58-84): record tokens and open every in-channel except
+// the one the first marker arrived on (arrive = -1 at the initiator).  A channel's
+// recording is the cursor interval [begin, end) over the tokens delivered on it.
+__device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, int32_t sid, int32_t arrive) {
   const ExecParams& p = x.p;
-  const Layout& lay = p.lay;
-  if (!CLSNAP_ABL_NOSTORE)
-    p.snap_tok[((int64_t)sid * p.n_nodes + w) * p.stride + ln.inst] = (int32_t)LW(lay.w_tok + w);
-  const int32_t k0 = x.t.in_off[w], k1 = x.t.in_off[w + 1];
-  for (int32_t k = k0; k < k1; ++k) {
-    const int32_t cc = x.t.in_ch[k];
-    const uint32_t td = LW(lay.w_chw + cc) >> 16;
-    if (!CLSNAP_ABL_NOSTORE)
-      p.snap_rec[((int64_t)sid * p.n_ch + cc) * p.stride + ln.inst] = cc == arrive ? (td | (td << 16)) : td;
+  const Layout& lay = x.lay;
+  p.snap_tok[((int64_t)sid * p.n_nodes + x.v) * p.stride + x.inst] = ln.tokens;
+  for (int32_t kj = 0; kj < x.indeg; ++kj) {
+    const uint32_t cur = PW(lay.w_cur + kj);
+    const uint32_t cc = PW(lay.w_int + kj) >> 16;
+    p.snap_rec[((int64_t)sid * p.n_ch + cc) * p.stride + x.inst] = kj == arrive ? (cur | (cur << 16)) : cur;
   }
 }
 
-// NotifyCompletedSnapshot (sim.go:126-131): global completion when all N nodes finished.
-__device__ __forceinline__ void node_complete(const ExecParams& p, Lane& ln, int32_t sid) {
-  const Layout& lay = p.lay;
-  const uint32_t di = lay.w_done + (sid >> 2);
-  const uint32_t sh = (sid & 3) * 8;
-  const uint32_t dw = LW(di);
-  const uint32_t n = ((dw >> sh) & 0xffu) + 1;
-  LW(di) = (dw & ~(0xffu << sh)) | (n << sh);
-  if (n == (uint32_t)p.n_nodes) {
-    if (!CLSNAP_ABL_NOSTORE) p.snap_tick[(int64_t)sid * p.stride + ln.inst] = ln.time;
-    ln.ndone++;
+__device__ __forceinline__ void set_pend(const Ctx& x, int32_t sid, uint32_t val) {
+  const uint32_t pi = x.lay.w_pend + (sid >> 2), sh = (sid & 3) * 8;
+  PW(pi) = (PW(pi) & ~(0xffu << sh)) | (val << sh);
+}
+
+// NotifyCompletedSnapshot (sim.go:126-131): the instance's snapshot completes when all N
+// nodes have; one LDS counter per (instance, snapshot).
+__device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
+  const uint32_t old = atomicAdd(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
+  if (old + 1 == (uint32_t)x.p.n_nodes) {
+    x.p.snap_tick[(int64_t)sid * x.p.stride + x.inst] = ln.time;
+    atomicAdd(&XW(x.lay.x_ndone + x.seg), 1u);
   }
 }
 
-// HandleMarker (node.go:149-171) at node w, arriving on channel c.
-__device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, int32_t w, int32_t c,
-                                              int32_t sid) {
-  const ExecParams& p = x.p;
-  const Layout& lay = p.lay;
-  const uint32_t st = LW(lay.w_started + w);
-  const uint32_t pi = lay.w_pend + w * lay.sp + (sid >> 2);
-  const uint32_t sh = (sid & 3) * 8;
-  const uint32_t pw = LW(pi);
-  int32_t pend;
-  if (!((st >> sid) & 1u)) {
-    LW(lay.w_started + w) = st | (1u << sid);
-    create_local(x, ln, w, sid, c);
-    pend = (x.t.in_off[w + 1] - x.t.in_off[w]) - 1;
-    broadcast_marker(x, ln, w, sid);
-  } else {
-    const uint32_t td = LW(lay.w_chw + c) >> 16;
-    if (!CLSNAP_ABL_NOSTORE)
-      reinterpret_cast<uint16_t*>(p.snap_rec)[2 * (((int64_t)sid * p.n_ch + c) * p.stride + ln.inst) + 1] =
-          (uint16_t)td;
-    pend = (int32_t)((pw >> sh) & 0xffu) - 1;
+// Fold lane-local engine failures into the instance status (all lanes must call).
+__device__ __forceinline__ void resolve_failures(const Ctx& x, Lane& ln) {
+  const uint64_t m = __ballot(ln.flag != 0) & x.seg_mask;
+  if (__builtin_expect(__ballot(m != 0) == 0, 1)) return;
+  const int32_t src = m ? (int32_t)__builtin_ctzll(m) : x.lane;
+  const int32_t code = __shfl(ln.flag, src);
+  if (m && ln.alive) {
+    ln.status = code;
+    ln.alive = false;
   }
-  LW(pi) = (pw & ~(0xffu << sh)) | ((uint32_t)pend << sh);
-  if (pend == 0) node_complete(p, ln, sid);
+  ln.flag = 0;
 }
 
-// Tick (sim.go:71-95).
-__device__ __forceinline__ void tick(const Ctx& x, Lane& ln) {
-  const ExecParams& p = x.p;
-  const Layout& lay = p.lay;
+// Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
+// Must be reached by all lanes of the wave.
+__device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
+  const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
-  ln.time++;
-  for (int32_t v = 0; v < p.n_nodes; ++v) {
-    const int32_t e0 = x.t.out_off[v], e1 = x.t.out_off[v + 1];
-    bool done = !ln.alive;
-    for (int32_t c = e0; c < e1; ++c) {
-      if (done) continue;
-      const uint32_t chw = LW(lay.w_chw + c);
+  // ---- A: pick ------------------------------------------------------------
+  uint32_t pick = 0, empty_scanned = 0;
+  if (act) {
+    ln.time++;
+    for (int32_t ko = 0; ko < x.outdeg; ++ko) {
+      const uint32_t chw = PW(lay.w_chw + ko);
       const uint32_t cnt = (chw >> 8) & 0xffu;
-      if (!cnt) continue;
+      if (!cnt) {
+        empty_scanned |= 1u << ko;
+        continue;
+      }
       ln.peek++;
       const uint32_t head = chw & 0xffu;
-      const uint32_t slot = lay.w_fifo + ((uint32_t)c << lay.cap_log2) + head;
-      const uint32_t e = LW(slot);
+      const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
+      const uint32_t e = PW(slot);
       if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) continue;
-      done = true;
-      const bool mk = (e & kMarkerBit) != 0;
       if (cnt > cap) {  // refill the freed slot (the new tail) from the HBM spill ring
+        const int64_t c = x.out_off + ko;
         const uint32_t om = (1u << lay.ocap_log2) - 1;
-        uint32_t* hp = &p.ovh[(int64_t)c * p.stride + ln.inst];
+        uint32_t* hp = &x.p.ovh[c * x.p.stride + x.inst];
         const uint32_t h = *hp;
-        LW(slot) = p.ovf[(((int64_t)c << lay.ocap_log2) + h) * p.stride + ln.inst];
+        PW(slot) = x.p.ovf[((c << lay.ocap_log2) + h) * x.p.stride + x.inst];
         *hp = (h + 1) & om;
       }
-      LW(lay.w_chw + c) = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1)) +
-                          (mk ? 0u : kTokDelivOne);
-      const int32_t w = x.t.ch_dst[c];
-      if (mk) {
-        ln.pop_mk++;
-        handle_marker(x, ln, w, c, (int32_t)(e & 0xffffu));
-      } else {
-        ln.pop_tok++;
-        LW(lay.w_tok + w) += e & 0xffffu;  // HandleToken: tokens += data
-      }
+      PW(lay.w_chw + ko) = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
+      pick = (e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16);
+      break;
     }
   }
+  XW(lay.x_pick + x.lane) = pick;
+  wave_sync();
+  // ---- B: receive, in ascending sender rank ---------------------------------
+  int32_t ntrig = 0;
+  if (act) {
+    for (int32_t ki = 0; ki < x.indeg; ++ki) {
+      const uint32_t it = PW(lay.w_int + ki);
+      const uint32_t src = it & 0xffu;
+      const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
+      if (!(pk & kPickValid) || ((pk >> 16) & 0x7fu) != ((it >> 8) & 0xffu)) continue;
+      const uint32_t pay = pk & 0xffffu;
+      if (!(pk & kMarkerBit)) {  // HandleToken: tokens += data; recording cursor advances
+        ln.pop_tok++;
+        ln.tokens += (int32_t)pay;
+        PW(lay.w_cur + ki) += 1u;
+        continue;
+      }
+      ln.pop_mk++;  // HandleMarker
+      const int32_t sid = (int32_t)pay;
+      const uint32_t sh = (sid & 3) * 8;
+      uint32_t pend;
+      if (!((ln.started >> sid) & 1u)) {
+        ln.started |= 1u << sid;
+        create_local(x, ln, sid, ki);
+        pend = (uint32_t)x.indeg - 1;
+        if (x.outdeg) {
+          XW(lay.x_tslot + x.seg_base + src) = (uint32_t)x.outdeg;
+          PW(lay.w_trig + ntrig) = src | ((uint32_t)sid << 8);
+          ntrig++;
+        }
+      } else {
+        reinterpret_cast<uint16_t*>(x.p.snap_rec)[2 * (((int64_t)sid * x.p.n_ch + (it >> 16)) * x.p.stride + x.inst) + 1] =
+            (uint16_t)PW(lay.w_cur + ki);
+        pend = ((PW(lay.w_pend + (sid >> 2)) >> sh) & 0xffu) - 1;
+      }
+      set_pend(x, sid, pend);
+      if (pend == 0) node_complete(x, ln, sid);
+    }
+  }
+  // ---- C/D: broadcast draws in sender order, then push -------------------------
+  if (__ballot(ntrig > 0)) {
+    wave_sync();
+    const uint32_t t = XW(lay.x_tslot + x.lane);
+    XW(lay.x_tslot + x.lane) = 0;
+    uint32_t incl = t;
+#pragma unroll
+    for (int32_t d = 1; d < kWave; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (x.lane >= d) incl += y;
+    }
+    const uint32_t before = __shfl(incl, x.seg_base > 0 ? x.seg_base - 1 : 0);
+    const uint32_t last = __shfl(incl, x.seg_base + x.p.n_nodes - 1);
+    const uint32_t base = x.seg_base > 0 ? before : 0;
+    XW(lay.x_off + x.lane) = incl - t - base;
+    wave_sync();
+    if (act) {
+      for (int32_t kk = 0; kk < ntrig; ++kk) {
+        const uint32_t tv = PW(lay.w_trig + kk);
+        const uint32_t src = tv & 0xffu;
+        const uint32_t sid = tv >> 8;
+        const int64_t k0 = (int64_t)ln.draw + XW(lay.x_off + x.seg_base + src);
+        for (int32_t j = 0; j < x.outdeg; ++j) {
+          push(x, ln, j, kMarkerBit | sid, k0 + j);
+          // the reference scans this sender's links after the push when the trigger came
+          // from a lower rank: a link that was empty at tick start gets peeked once more
+          if ((int32_t)src < x.v && ((empty_scanned >> j) & 1u)) {
+            ln.peek++;
+            empty_scanned &= ~(1u << j);
+          }
+        }
+      }
+      ln.draw += (int32_t)(last - base);
+    }
+  }
+  resolve_failures(x, ln);
 }
 
-__global__ __launch_bounds__(64) void cl_exec_kernel(ExecParams p, const int32_t* __restrict__ topo,
-                                                     const Op* __restrict__ ops,
-                                                     const uint8_t* __restrict__ sched) {
+__global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
+                                                                         const Op* __restrict__ ops,
+                                                                         const uint8_t* __restrict__ sched) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const int32_t N = p.n_nodes, C = p.n_ch;
-  const Ctx x{p, TopoView{topo, topo + (N + 1), topo + (N + 1) + C, topo + 2 * (N + 1) + C,
-                          topo + 2 * (N + 1) + 2 * C},
-              sched};
-  Lane ln;
-  const int lane = threadIdx.x;
-  ln.L = lds + lane;
-  ln.inst = (int64_t)blockIdx.x * kWave + lane;
-  const bool valid = ln.inst < p.n_inst;
   const Layout& lay = p.lay;
+  const int32_t N = p.n_nodes;
+  const int32_t lane = threadIdx.x & (kWave - 1);
+  const int32_t wib = threadIdx.x / kWave;
+  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wib;
+  uint32_t* X = lds + (size_t)wib * lay.wave_words;
+  const int32_t seg = lane / N;
+  const int32_t v = lane - seg * N;
+  const int64_t inst = wave * lay.ipw + seg;
+  const bool valid = seg < lay.ipw && inst < p.n_inst;
+  const int64_t ii = valid ? inst : 0;  // safe index for lanes without an instance
+  const uint32_t* nb = topo + (size_t)v * (3 + lay.id);
+  const int32_t indeg = valid ? (int32_t)nb[0] : 0;
+  const int32_t outdeg = valid ? (int32_t)nb[1] : 0;
+  const uint64_t seg_mask = N == 64 ? ~0ull : (((1ull << N) - 1) << (seg * N));
+  const Ctx x{p, lay, X + lane, X, sched + ii * p.sched_row, lane, seg * N, v, seg, ii, seg_mask,
+              indeg, outdeg, valid ? (int32_t)nb[2] : 0};
 
+  Lane ln;
+  ln.flag = 0;
+  for (int32_t k = lane; k < lay.shared; k += kWave) XW(lay.priv * kWave + k) = 0u;
+  const int64_t st = p.stride;
   if (p.fresh) {
-    for (int32_t k = 0; k < lay.words; ++k) LW(k) = 0u;
-    for (int32_t v = 0; v < p.n_nodes; ++v) LW(lay.w_tok + v) = (uint32_t)x.t.init_tok[v];
-    ln.time = ln.dptr = ln.status = ln.ndone = 0;
+    for (int32_t k = 0; k < lay.priv; ++k) PW(k) = 0u;
+    ln.tokens = valid ? (int32_t)topo[(size_t)N * (3 + lay.id) + v] : 0;
+    ln.started = 0;
+    ln.time = ln.draw = ln.status = 0;
     ln.peek = ln.pop_tok = ln.pop_mk = ln.push = 0;
   } else {
-    for (int32_t k = 0; k < lay.words; ++k) LW(k) = p.state[(int64_t)k * p.stride + ln.inst];
-    const int32_t* r = p.regs + ln.inst;
-    ln.time = r[R_TIME * p.stride];
-    ln.dptr = r[R_DRAW * p.stride];
-    ln.status = r[R_STATUS * p.stride];
-    ln.ndone = r[R_NDONE * p.stride];
-    ln.peek = (uint32_t)r[R_PEEK * p.stride];
-    ln.pop_tok = (uint32_t)r[R_POP_TOK * p.stride];
-    ln.pop_mk = (uint32_t)r[R_POP_MK * p.stride];
-    ln.push = (uint32_t)r[R_PUSH * p.stride];
+    const uint32_t* S = p.state + ii;
+    const int32_t b = v * (lay.priv + G_NUM);
+    for (int32_t k = 0; k < lay.priv; ++k) PW(k) = valid ? S[(b + k) * st] : 0u;
+    const uint32_t* R = S + (int64_t)(b + lay.priv) * st;
+    ln.tokens = valid ? (int32_t)R[G_TOKENS * st] : 0;
+    ln.started = valid ? R[G_STARTED * st] : 0;
+    ln.time = valid ? (int32_t)R[G_TIME * st] : 0;
+    ln.draw = valid ? (int32_t)R[G_DRAW * st] : 0;
+    ln.status = valid ? (int32_t)R[G_STATUS * st] : 0;
+    ln.peek = valid ? R[G_PEEK * st] : 0;
+    ln.pop_tok = valid ? R[G_POP_TOK * st] : 0;
+    ln.pop_mk = valid ? R[G_POP_MK * st] : 0;
+    ln.push = valid ? R[G_PUSH * st] : 0;
+    wave_sync();
+    if (valid && v == 0) {
+      const uint32_t* D = S + (int64_t)N * (lay.priv + G_NUM) * st;
+      for (int32_t s = 0; s < lay.s_cap; ++s) XW(lay.x_done + seg * lay.s_cap + s) = D[s * st];
+      XW(lay.x_ndone + seg) = D[lay.s_cap * st];
+    }
   }
+  for (int32_t k = 0; k < indeg; ++k) PW(lay.w_int + k) = nb[3 + k];
+  wave_sync();
   ln.alive = valid && ln.status == ST_OK;
-  if (ln.alive) open_window(x, ln);
   int32_t n_started = p.n_started_before;
 
   for (int32_t i = p.op_begin; i < p.op_end; ++i) {
     const Op op = ops[i];
     if (op.kind == OP_SEND) {
-      // SendTokens: balance check, then link lookup, then push (node.go:113-130)
-      if (ln.alive) {
-        const int32_t t = (int32_t)LW(lay.w_tok + op.a);
-        if (t < op.c) {
-          fail(ln, ST_FATAL_INSUFFICIENT);
-        } else if (op.b < 0) {
-          fail(ln, ST_FATAL_UNKNOWN_DEST);
-        } else {
-          LW(lay.w_tok + op.a) = (uint32_t)(t - op.c);
-          push(x, ln, op.b, (uint32_t)op.c);
+      // SendTokens (node.go:112-131): balance check, link lookup, push -- all at src
+      int32_t f = 0;
+      if (ln.alive && v == op.a) {
+        if (ln.tokens < op.c) f = ST_FATAL_INSUFFICIENT;
+        else if (op.b < 0) f = ST_FATAL_UNKNOWN_DEST;
+        else {
+          ln.tokens -= op.c;
+          push(x, ln, op.b, (uint32_t)op.c, ln.draw);
         }
       }
-    } else if (op.kind == OP_SNAP) {
-      // sim.StartSnapshot -> node.StartSnapshot: initiator records every in-channel
+      const int32_t fs = __shfl(f, x.seg_base + op.a);
       if (ln.alive) {
-        const int32_t v = op.a, sid = op.b;
-        LW(lay.w_started + v) |= 1u << sid;
-        create_local(x, ln, v, sid, -1);
-        const uint32_t pi = lay.w_pend + v * lay.sp + (sid >> 2);
-        const uint32_t sh = (sid & 3) * 8;
-        const uint32_t indeg = (uint32_t)(x.t.in_off[v + 1] - x.t.in_off[v]);
-        LW(pi) = (LW(pi) & ~(0xffu << sh)) | (indeg << sh);
-        broadcast_marker(x, ln, v, sid);
+        if (fs) {
+          ln.status = fs;
+          ln.alive = false;
+        } else {
+          ln.draw += 1;
+        }
       }
+      resolve_failures(x, ln);
+    } else if (op.kind == OP_SNAP) {
+      // sim.StartSnapshot -> node.StartSnapshot: the initiator records every in-channel
+      if (ln.alive && v == op.a) {
+        ln.started |= 1u << op.b;
+        create_local(x, ln, op.b, -1);
+        set_pend(x, op.b, (uint32_t)indeg);
+        for (int32_t j = 0; j < outdeg; ++j) push(x, ln, j, kMarkerBit | (uint32_t)op.b, (int64_t)ln.draw + j);
+      }
+      if (ln.alive) ln.draw += op.c;
       n_started++;
+      resolve_failures(x, ln);
     } else if (op.kind == OP_TICK) {
-      for (int32_t k = 0; k < op.a; ++k)
-        if (ln.alive) tick(x, ln);
+      for (int32_t k = 0; k < op.a; ++k) {
+        if (!__ballot(ln.alive)) break;
+        tick(x, ln, ln.alive);
+      }
     } else if (op.kind == OP_DRAIN) {
       // tick until every started snapshot completed (per instance), then op.b more
       for (int32_t dt = 0;; ++dt) {
-        const bool need = ln.alive && ln.ndone < n_started;
-        if (!__any(need)) break;
-        if (need) {
-          if (dt >= op.a) fail(ln, ST_HANG);
-          else tick(x, ln);
+        const bool need = ln.alive && (int32_t)XW(lay.x_ndone + seg) < n_started;
+        if (!__ballot(need)) break;
+        if (need && dt >= op.a) {
+          ln.status = ST_HANG;
+          ln.alive = false;
         }
+        tick(x, ln, need && ln.alive);
       }
-      for (int32_t k = 0; k < op.b; ++k)
-        if (ln.alive) tick(x, ln);
+      for (int32_t k = 0; k < op.b; ++k) {
+        if (!__ballot(ln.alive)) break;
+        tick(x, ln, ln.alive);
+      }
     }
   }
 
-  // tokens still queued (the checkTokens residual, test_common.go:298-328)
+  // ---- epilogue: tokens still queued, per-instance sums, state image -----------
   int32_t inflight = 0;
   {
     const uint32_t cap = 1u << lay.cap_log2;
-    for (int32_t c = 0; c < p.n_ch; ++c) {
-      const uint32_t chw = LW(lay.w_chw + c);
+    for (int32_t ko = 0; ko < outdeg; ++ko) {
+      const uint32_t chw = PW(lay.w_chw + ko);
       const uint32_t cnt = (chw >> 8) & 0xffu, head = chw & 0xffu;
       for (uint32_t k = 0; k < cnt && k < cap; ++k) {
-        const uint32_t e = LW(lay.w_fifo + ((uint32_t)c << lay.cap_log2) + ((head + k) & (cap - 1)));
+        const uint32_t e = PW(lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + ((head + k) & (cap - 1)));
         if (!(e & kMarkerBit)) inflight += (int32_t)(e & 0xffffu);
       }
       if (cnt > cap) {
+        const int64_t c = x.out_off + ko;
         const uint32_t om = (1u << lay.ocap_log2) - 1;
-        const uint32_t h = p.ovh[(int64_t)c * p.stride + ln.inst];
+        const uint32_t h = p.ovh[c * st + ii];
         for (uint32_t k = 0; k < cnt - cap; ++k) {
-          const uint32_t e = p.ovf[(((int64_t)c << lay.ocap_log2) + ((h + k) & om)) * p.stride + ln.inst];
+          const uint32_t e = p.ovf[((c << lay.ocap_log2) + ((h + k) & om)) * st + ii];
           if (!(e & kMarkerBit)) inflight += (int32_t)(e & 0xffffu);
         }
       }
     }
   }
-
   if (valid) {
-    for (int32_t k = 0; k < lay.words; ++k) p.state[(int64_t)k * p.stride + ln.inst] = LW(k);
-    int32_t* r = p.regs + ln.inst;
-    r[R_TIME * p.stride] = ln.time;
-    r[R_DRAW * p.stride] = ln.dptr;
-    r[R_STATUS * p.stride] = ln.status;
-    r[R_NDONE * p.stride] = ln.ndone;
-    r[R_PEEK * p.stride] = (int32_t)ln.peek;
-    r[R_POP_TOK * p.stride] = (int32_t)ln.pop_tok;
-    r[R_POP_MK * p.stride] = (int32_t)ln.pop_mk;
-    r[R_PUSH * p.stride] = (int32_t)ln.push;
-    r[R_INFLIGHT_TOK * p.stride] = inflight;
+    uint32_t* acc = &XW(lay.x_acc + 5 * seg);
+    atomicAdd(acc + 0, ln.peek);
+    atomicAdd(acc + 1, ln.pop_tok);
+    atomicAdd(acc + 2, ln.pop_mk);
+    atomicAdd(acc + 3, ln.push);
+    atomicAdd(acc + 4, (uint32_t)inflight);
+  }
+  wave_sync();
+  if (!valid) return;
+  p.fin_tok[(int64_t)v * st + ii] = ln.tokens;
+  uint32_t* S = p.state + ii;
+  const int32_t b = v * (lay.priv + G_NUM);
+  for (int32_t k = 0; k < lay.priv; ++k) S[(b + k) * st] = PW(k);
+  uint32_t* R = S + (int64_t)(b + lay.priv) * st;
+  R[G_TOKENS * st] = (uint32_t)ln.tokens;
+  R[G_STARTED * st] = ln.started;
+  R[G_TIME * st] = (uint32_t)ln.time;
+  R[G_DRAW * st] = (uint32_t)ln.draw;
+  R[G_STATUS * st] = (uint32_t)ln.status;
+  R[G_PEEK * st] = ln.peek;
+  R[G_POP_TOK * st] = ln.pop_tok;
+  R[G_POP_MK * st] = ln.pop_mk;
+  R[G_PUSH * st] = ln.push;
+  if (v == 0) {
+    uint32_t* D = S + (int64_t)N * (lay.priv + G_NUM) * st;
+    for (int32_t s = 0; s < lay.s_cap; ++s) D[s * st] = XW(lay.x_done + seg * lay.s_cap + s);
+    D[lay.s_cap * st] = XW(lay.x_ndone + seg);
+    const uint32_t* acc = &XW(lay.x_acc + 5 * seg);
+    int32_t* r = p.regs + ii;
+    r[R_TIME * st] = ln.time;
+    r[R_DRAW * st] = ln.draw;
+    r[R_STATUS * st] = ln.status;
+    r[R_NDONE * st] = (int32_t)XW(lay.x_ndone + seg);
+    r[R_PEEK * st] = (int32_t)acc[0];
+    r[R_POP_TOK * st] = (int32_t)acc[1];
+    r[R_POP_MK * st] = (int32_t)acc[2];
+    r[R_PUSH * st] = (int32_t)acc[3];
+    r[R_INFLIGHT_TOK * st] = (int32_t)acc[4];
   }
 }
 
-#undef LW
+#undef PW
+#undef XW
 
 // Per-instance snapshot hash / conservation checks, summed over the batch.
 __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
@@ -395,8 +468,7 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
     v[6] = cut;
     v[8] = (unsigned long long)ncomplete;
     int64_t fin = inflight;
-    for (int32_t n = 0; n < p.n_nodes; ++n)
-      fin += (int32_t)p.state[(int64_t)(p.lay.w_tok + n) * p.stride + inst];
+    for (int32_t n = 0; n < p.n_nodes; ++n) fin += p.fin_tok[(int64_t)n * p.stride + inst];
     const int64_t d = fin - p.total_tokens;
     v[7] = (unsigned long long)(d < 0 ? -d : d);
   }
@@ -406,16 +478,17 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
 
 }  // namespace
 
-int launch_exec(const ExecParams& p, const int32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
-  const size_t lds = (size_t)p.lay.words * kWave * sizeof(uint32_t);
+int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
+  const size_t lds = (size_t)p.lay.wave_words * kWavesPerBlock * sizeof(uint32_t);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
-  const unsigned blocks = (unsigned)(p.stride / kWave);
-  hipLaunchKernelGGL(cl_exec_kernel, dim3(blocks), dim3(kWave), lds, (hipStream_t)stream, p, topo, ops,
-                     sched);
+  const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
+  const unsigned blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+  hipLaunchKernelGGL(cl_exec_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, p,
+                     topo, ops, sched);
   return (int)hipGetLastError();
 }
 
