@@ -76,7 +76,8 @@ def main():
         torch.cuda.synchronize()
 
     cl = importlib.import_module(PKG)
-    seed_base = cl.REFERENCE_SEED + rank * per_gpu
+    cldist = importlib.import_module(PKG + ".dist")
+    _, seed_base = cldist.shard(per_gpu, rank, cl.REFERENCE_SEED)
     sim = cl.ChandyLamportSim(per_gpu, device=local_rank, seed_base=seed_base,
                               fifo_lds_slots=args.fifo_slots)
     sim.read_topology_file(os.path.join(TEST_DATA, top))
@@ -101,15 +102,10 @@ def main():
     k_total_ms, k_launches = sim.kernel_time()   # HIP events around each timed launch
 
     sums = sim.checksums()
-    t_local = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    s_local = torch.tensor(sums.tolist() + [counters_ok["pop_tok"] + counters_ok["pop_mk"]],
-                           dtype=torch.int64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t_local, op=dist.ReduceOp.MAX)
-        dist.all_reduce(s_local, op=dist.ReduceOp.SUM)
-    t_max = float(t_local.item())
-    tot = dict(zip(cl.SUM_NAMES, s_local.tolist()[:len(cl.SUM_NAMES)]))
-    delivered_ok = s_local.tolist()[-1]          # packets of OK instances, all ranks
+    t_max, red = cldist.reduce_results(elapsed, sums.tolist() + [counters_ok["pop_tok"] + counters_ok["pop_mk"]],
+                                       "cuda")   # RCCL all-reduce (max time, summed checksums)
+    tot = dict(zip(cl.SUM_NAMES, red[:len(cl.SUM_NAMES)]))
+    delivered_ok = red[-1]                       # packets of OK instances, all ranks
 
     per_step = t_max / args.steps
     value = delivered_ok / per_step

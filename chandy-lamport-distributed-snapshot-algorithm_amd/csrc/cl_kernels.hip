@@ -35,6 +35,8 @@
 namespace clsnap {
 namespace {
 
+// Uniform-per-lane context.  Output arrays are addressed with 32-bit element indices
+// (the host keeps every array below 2^32 elements).
 struct Ctx {
   const ExecParams& p;
   const Layout& lay;
@@ -42,7 +44,8 @@ struct Ctx {
   uint32_t* X;  // this wave's LDS base (shared region at lay.x_*)
   const uint8_t* __restrict__ row;  // this instance's delay row
   int32_t lane, seg_base, v, seg;
-  int64_t inst;
+  uint32_t inst;      // instance index (0 for lanes without an instance)
+  uint32_t stride;    // instance stride of every [k][stride] array
   uint64_t seg_mask;  // the instance's lanes
   int32_t indeg, outdeg, out_off;
 };
@@ -65,6 +68,17 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Inclusive prefix sum over the 64 lanes with DPP (row shifts, then row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
 // Queue.Push (queue.go:18-20) on out-link ko; receiveTime = time + 1 + draw (sim.go:101).
 // `k` is the index of the draw in this instance's delay stream.
 __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int64_t k) {
@@ -80,10 +94,10 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
     PW(lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + ((chw + cnt) & (cap - 1))) = e;
   } else {  // LDS ring full: younger packets of this channel spill to an HBM ring
     if (lay.ocap_log2 < 0 || cnt - cap >= (1u << lay.ocap_log2)) { ln.flag = ST_FIFO_OVERFLOW; return; }
-    const int64_t c = x.out_off + ko;
+    const uint32_t c = (uint32_t)(x.out_off + ko);
     const uint32_t om = (1u << lay.ocap_log2) - 1;
-    const uint32_t h = x.p.ovh[c * x.p.stride + x.inst];
-    x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.p.stride + x.inst] = e;
+    const uint32_t h = x.p.ovh[c * x.stride + x.inst];
+    x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.stride + x.inst] = e;
   }
   PW(lay.w_chw + ko) = chw + kCountOne;
   ln.push++;
@@ -92,14 +106,18 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
 // CreateLocalSnapshot (node.go:58-84): record tokens and open every in-channel except
 // the one the first marker arrived on (arrive = -1 at the initiator).  A channel's
 // recording is the cursor interval [begin, end) over the tokens delivered on it.
+template <int D>
 __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, int32_t sid, int32_t arrive) {
   const ExecParams& p = x.p;
   const Layout& lay = x.lay;
-  p.snap_tok[((int64_t)sid * p.n_nodes + x.v) * p.stride + x.inst] = ln.tokens;
-  for (int32_t kj = 0; kj < x.indeg; ++kj) {
-    const uint32_t cur = PW(lay.w_cur + kj);
-    const uint32_t cc = PW(lay.w_int + kj) >> 16;
-    p.snap_rec[((int64_t)sid * p.n_ch + cc) * p.stride + x.inst] = kj == arrive ? (cur | (cur << 16)) : cur;
+  p.snap_tok[((uint32_t)sid * p.n_nodes + x.v) * x.stride + x.inst] = ln.tokens;
+#pragma unroll
+  for (int32_t kj = 0; kj < D; ++kj) {
+    if (kj < x.indeg) {
+      const uint32_t cur = PW(lay.w_cur + kj);
+      const uint32_t cc = PW(lay.w_int + kj) >> 16;
+      p.snap_rec[((uint32_t)sid * p.n_ch + cc) * x.stride + x.inst] = kj == arrive ? (cur | (cur << 16)) : cur;
+    }
   }
 }
 
@@ -113,15 +131,15 @@ __device__ __forceinline__ void set_pend(const Ctx& x, int32_t sid, uint32_t val
 __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
   const uint32_t old = atomicAdd(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
   if (old + 1 == (uint32_t)x.p.n_nodes) {
-    x.p.snap_tick[(int64_t)sid * x.p.stride + x.inst] = ln.time;
+    x.p.snap_tick[(uint32_t)sid * x.stride + x.inst] = ln.time;
     atomicAdd(&XW(x.lay.x_ndone + x.seg), 1u);
   }
 }
 
 // Fold lane-local engine failures into the instance status (all lanes must call).
 __device__ __forceinline__ void resolve_failures(const Ctx& x, Lane& ln) {
+  if (__builtin_expect(__ballot(ln.flag != 0) == 0, 1)) return;
   const uint64_t m = __ballot(ln.flag != 0) & x.seg_mask;
-  if (__builtin_expect(__ballot(m != 0) == 0, 1)) return;
   const int32_t src = m ? (int32_t)__builtin_ctzll(m) : x.lane;
   const int32_t code = __shfl(ln.flag, src);
   if (m && ln.alive) {
@@ -132,7 +150,8 @@ __device__ __forceinline__ void resolve_failures(const Ctx& x, Lane& ln) {
 }
 
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
-// Must be reached by all lanes of the wave.
+// Must be reached by all lanes of the wave.  D bounds every node's in/out degree.
+template <int D>
 __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
@@ -140,7 +159,10 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
   uint32_t pick = 0, empty_scanned = 0;
   if (act) {
     ln.time++;
-    for (int32_t ko = 0; ko < x.outdeg; ++ko) {
+    bool done = false;
+#pragma unroll
+    for (int32_t ko = 0; ko < D; ++ko) {
+      if (done || ko >= x.outdeg) continue;
       const uint32_t chw = PW(lay.w_chw + ko);
       const uint32_t cnt = (chw >> 8) & 0xffu;
       if (!cnt) {
@@ -153,16 +175,16 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
       const uint32_t e = PW(slot);
       if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) continue;
       if (cnt > cap) {  // refill the freed slot (the new tail) from the HBM spill ring
-        const int64_t c = x.out_off + ko;
+        const uint32_t c = (uint32_t)(x.out_off + ko);
         const uint32_t om = (1u << lay.ocap_log2) - 1;
-        uint32_t* hp = &x.p.ovh[c * x.p.stride + x.inst];
+        uint32_t* hp = &x.p.ovh[c * x.stride + x.inst];
         const uint32_t h = *hp;
-        PW(slot) = x.p.ovf[((c << lay.ocap_log2) + h) * x.p.stride + x.inst];
+        PW(slot) = x.p.ovf[((c << lay.ocap_log2) + h) * x.stride + x.inst];
         *hp = (h + 1) & om;
       }
       PW(lay.w_chw + ko) = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
       pick = (e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16);
-      break;
+      done = true;
     }
   }
   XW(lay.x_pick + x.lane) = pick;
@@ -170,7 +192,9 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
   if (act) {
-    for (int32_t ki = 0; ki < x.indeg; ++ki) {
+#pragma unroll
+    for (int32_t ki = 0; ki < D; ++ki) {
+      if (ki >= x.indeg) continue;
       const uint32_t it = PW(lay.w_int + ki);
       const uint32_t src = it & 0xffu;
       const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
@@ -188,7 +212,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
       uint32_t pend;
       if (!((ln.started >> sid) & 1u)) {
         ln.started |= 1u << sid;
-        create_local(x, ln, sid, ki);
+        create_local<D>(x, ln, sid, ki);
         pend = (uint32_t)x.indeg - 1;
         if (x.outdeg) {
           XW(lay.x_tslot + x.seg_base + src) = (uint32_t)x.outdeg;
@@ -196,7 +220,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
           ntrig++;
         }
       } else {
-        reinterpret_cast<uint16_t*>(x.p.snap_rec)[2 * (((int64_t)sid * x.p.n_ch + (it >> 16)) * x.p.stride + x.inst) + 1] =
+        reinterpret_cast<uint16_t*>(x.p.snap_rec)[2 * (((uint32_t)sid * x.p.n_ch + (it >> 16)) * x.stride + x.inst) + 1] =
             (uint16_t)PW(lay.w_cur + ki);
         pend = ((PW(lay.w_pend + (sid >> 2)) >> sh) & 0xffu) - 1;
       }
@@ -209,24 +233,20 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
     wave_sync();
     const uint32_t t = XW(lay.x_tslot + x.lane);
     XW(lay.x_tslot + x.lane) = 0;
-    uint32_t incl = t;
-#pragma unroll
-    for (int32_t d = 1; d < kWave; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d);
-      if (x.lane >= d) incl += y;
-    }
-    const uint32_t before = __shfl(incl, x.seg_base > 0 ? x.seg_base - 1 : 0);
-    const uint32_t last = __shfl(incl, x.seg_base + x.p.n_nodes - 1);
-    const uint32_t base = x.seg_base > 0 ? before : 0;
-    XW(lay.x_off + x.lane) = incl - t - base;
+    const uint32_t incl = wave_incl_scan(t);
+    XW(lay.x_off + x.lane) = incl;
     wave_sync();
+    const uint32_t base = x.seg_base > 0 ? XW(lay.x_off + x.seg_base - 1) : 0u;
     if (act) {
       for (int32_t kk = 0; kk < ntrig; ++kk) {
         const uint32_t tv = PW(lay.w_trig + kk);
         const uint32_t src = tv & 0xffu;
         const uint32_t sid = tv >> 8;
-        const int64_t k0 = (int64_t)ln.draw + XW(lay.x_off + x.seg_base + src);
-        for (int32_t j = 0; j < x.outdeg; ++j) {
+        // exclusive prefix of the triggering sender within the instance
+        const int64_t k0 = (int64_t)ln.draw + (XW(lay.x_off + x.seg_base + src) - (uint32_t)x.outdeg - base);
+#pragma unroll
+        for (int32_t j = 0; j < D; ++j) {
+          if (j >= x.outdeg) continue;
           push(x, ln, j, kMarkerBit | sid, k0 + j);
           // the reference scans this sender's links after the push when the trigger came
           // from a lower rank: a link that was empty at tick start gets peeked once more
@@ -236,12 +256,13 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
           }
         }
       }
-      ln.draw += (int32_t)(last - base);
+      ln.draw += (int32_t)(XW(lay.x_off + x.seg_base + x.p.n_nodes - 1) - base);
     }
   }
   resolve_failures(x, ln);
 }
 
+template <int D>
 __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
                                                                          const Op* __restrict__ ops,
                                                                          const uint8_t* __restrict__ sched) {
@@ -250,24 +271,24 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
   const int32_t N = p.n_nodes;
   const int32_t lane = threadIdx.x & (kWave - 1);
   const int32_t wib = threadIdx.x / kWave;
-  const int64_t wave = (int64_t)blockIdx.x * kWavesPerBlock + wib;
+  const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
   uint32_t* X = lds + (size_t)wib * lay.wave_words;
   const int32_t seg = lane / N;
   const int32_t v = lane - seg * N;
-  const int64_t inst = wave * lay.ipw + seg;
+  const uint32_t inst = wave * (uint32_t)lay.ipw + seg;
   const bool valid = seg < lay.ipw && inst < p.n_inst;
-  const int64_t ii = valid ? inst : 0;  // safe index for lanes without an instance
+  const uint32_t ii = valid ? inst : 0u;  // safe index for lanes without an instance
   const uint32_t* nb = topo + (size_t)v * (3 + lay.id);
   const int32_t indeg = valid ? (int32_t)nb[0] : 0;
   const int32_t outdeg = valid ? (int32_t)nb[1] : 0;
   const uint64_t seg_mask = N == 64 ? ~0ull : (((1ull << N) - 1) << (seg * N));
-  const Ctx x{p, lay, X + lane, X, sched + ii * p.sched_row, lane, seg * N, v, seg, ii, seg_mask,
+  const uint32_t st = (uint32_t)p.stride;
+  const Ctx x{p, lay, X + lane, X, sched + (size_t)ii * p.sched_row, lane, seg * N, v, seg, ii, st, seg_mask,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0};
 
   Lane ln;
   ln.flag = 0;
   for (int32_t k = lane; k < lay.shared; k += kWave) XW(lay.priv * kWave + k) = 0u;
-  const int64_t st = p.stride;
   if (p.fresh) {
     for (int32_t k = 0; k < lay.priv; ++k) PW(k) = 0u;
     ln.tokens = valid ? (int32_t)topo[(size_t)N * (3 + lay.id) + v] : 0;
@@ -276,9 +297,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
     ln.peek = ln.pop_tok = ln.pop_mk = ln.push = 0;
   } else {
     const uint32_t* S = p.state + ii;
-    const int32_t b = v * (lay.priv + G_NUM);
+    const uint32_t b = (uint32_t)v * (lay.priv + G_NUM);
     for (int32_t k = 0; k < lay.priv; ++k) PW(k) = valid ? S[(b + k) * st] : 0u;
-    const uint32_t* R = S + (int64_t)(b + lay.priv) * st;
+    const uint32_t* R = S + (b + lay.priv) * st;
     ln.tokens = valid ? (int32_t)R[G_TOKENS * st] : 0;
     ln.started = valid ? R[G_STARTED * st] : 0;
     ln.time = valid ? (int32_t)R[G_TIME * st] : 0;
@@ -290,9 +311,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
     ln.push = valid ? R[G_PUSH * st] : 0;
     wave_sync();
     if (valid && v == 0) {
-      const uint32_t* D = S + (int64_t)N * (lay.priv + G_NUM) * st;
-      for (int32_t s = 0; s < lay.s_cap; ++s) XW(lay.x_done + seg * lay.s_cap + s) = D[s * st];
-      XW(lay.x_ndone + seg) = D[lay.s_cap * st];
+      const uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
+      for (int32_t s = 0; s < lay.s_cap; ++s) XW(lay.x_done + seg * lay.s_cap + s) = Dn[s * st];
+      XW(lay.x_ndone + seg) = Dn[lay.s_cap * st];
     }
   }
   for (int32_t k = 0; k < indeg; ++k) PW(lay.w_int + k) = nb[3 + k];
@@ -327,32 +348,32 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
       // sim.StartSnapshot -> node.StartSnapshot: the initiator records every in-channel
       if (ln.alive && v == op.a) {
         ln.started |= 1u << op.b;
-        create_local(x, ln, op.b, -1);
+        create_local<D>(x, ln, op.b, -1);
         set_pend(x, op.b, (uint32_t)indeg);
-        for (int32_t j = 0; j < outdeg; ++j) push(x, ln, j, kMarkerBit | (uint32_t)op.b, (int64_t)ln.draw + j);
+#pragma unroll
+        for (int32_t j = 0; j < D; ++j)
+          if (j < outdeg) push(x, ln, j, kMarkerBit | (uint32_t)op.b, (int64_t)ln.draw + j);
       }
       if (ln.alive) ln.draw += op.c;
       n_started++;
       resolve_failures(x, ln);
-    } else if (op.kind == OP_TICK) {
-      for (int32_t k = 0; k < op.a; ++k) {
-        if (!__ballot(ln.alive)) break;
-        tick(x, ln, ln.alive);
-      }
-    } else if (op.kind == OP_DRAIN) {
-      // tick until every started snapshot completed (per instance), then op.b more
+    } else if (op.kind == OP_TICK || op.kind == OP_DRAIN) {
+      // TICK: op.a ticks.  DRAIN: tick until every started snapshot completed (at most
+      // op.a ticks, else HANG), then op.b more (test_common.go:123-137).  Per instance.
+      const bool drain = op.kind == OP_DRAIN;
+      int32_t rem = drain ? op.b : op.a;
+      bool waiting = drain;
       for (int32_t dt = 0;; ++dt) {
-        const bool need = ln.alive && (int32_t)XW(lay.x_ndone + seg) < n_started;
-        if (!__ballot(need)) break;
-        if (need && dt >= op.a) {
+        if (waiting && (!ln.alive || (int32_t)XW(lay.x_ndone + seg) >= n_started)) waiting = false;
+        if (waiting && dt >= op.a) {
           ln.status = ST_HANG;
           ln.alive = false;
+          waiting = false;
         }
-        tick(x, ln, need && ln.alive);
-      }
-      for (int32_t k = 0; k < op.b; ++k) {
-        if (!__ballot(ln.alive)) break;
-        tick(x, ln, ln.alive);
+        const bool act = ln.alive && (waiting || rem > 0);
+        if (!__ballot(act)) break;
+        tick<D>(x, ln, act);
+        if (act && !waiting) rem--;
       }
     }
   }
@@ -369,7 +390,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
         if (!(e & kMarkerBit)) inflight += (int32_t)(e & 0xffffu);
       }
       if (cnt > cap) {
-        const int64_t c = x.out_off + ko;
+        const uint32_t c = (uint32_t)(x.out_off + ko);
         const uint32_t om = (1u << lay.ocap_log2) - 1;
         const uint32_t h = p.ovh[c * st + ii];
         for (uint32_t k = 0; k < cnt - cap; ++k) {
@@ -389,11 +410,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
   }
   wave_sync();
   if (!valid) return;
-  p.fin_tok[(int64_t)v * st + ii] = ln.tokens;
+  p.fin_tok[(uint32_t)v * st + ii] = ln.tokens;
   uint32_t* S = p.state + ii;
-  const int32_t b = v * (lay.priv + G_NUM);
+  const uint32_t b = (uint32_t)v * (lay.priv + G_NUM);
   for (int32_t k = 0; k < lay.priv; ++k) S[(b + k) * st] = PW(k);
-  uint32_t* R = S + (int64_t)(b + lay.priv) * st;
+  uint32_t* R = S + (b + lay.priv) * st;
   R[G_TOKENS * st] = (uint32_t)ln.tokens;
   R[G_STARTED * st] = ln.started;
   R[G_TIME * st] = (uint32_t)ln.time;
@@ -404,9 +425,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
   R[G_POP_MK * st] = ln.pop_mk;
   R[G_PUSH * st] = ln.push;
   if (v == 0) {
-    uint32_t* D = S + (int64_t)N * (lay.priv + G_NUM) * st;
-    for (int32_t s = 0; s < lay.s_cap; ++s) D[s * st] = XW(lay.x_done + seg * lay.s_cap + s);
-    D[lay.s_cap * st] = XW(lay.x_ndone + seg);
+    uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
+    for (int32_t s = 0; s < lay.s_cap; ++s) Dn[s * st] = XW(lay.x_done + seg * lay.s_cap + s);
+    Dn[lay.s_cap * st] = XW(lay.x_ndone + seg);
     const uint32_t* acc = &XW(lay.x_acc + 5 * seg);
     int32_t* r = p.regs + ii;
     r[R_TIME * st] = ln.time;
@@ -478,18 +499,32 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
 
 }  // namespace
 
-int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
+template <int D>
+int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
   const size_t lds = (size_t)p.lay.wave_words * kWavesPerBlock * sizeof(uint32_t);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes);
+    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
   const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
   const unsigned blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL(cl_exec_kernel, dim3(blocks), dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, p,
+  hipLaunchKernelGGL(cl_exec_kernel<D>, dim3(blocks), dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, p,
                      topo, ops, sched);
   return (int)hipGetLastError();
+}
+
+// The kernel is instantiated for degree bounds 1, 2, 4, 8, 16, 32, 64, 128.
+int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
+  const int32_t d = p.lay.od > p.lay.id ? p.lay.od : p.lay.id;
+  if (d <= 1) return launch_exec_d<1>(p, topo, ops, sched, stream);
+  if (d <= 2) return launch_exec_d<2>(p, topo, ops, sched, stream);
+  if (d <= 4) return launch_exec_d<4>(p, topo, ops, sched, stream);
+  if (d <= 8) return launch_exec_d<8>(p, topo, ops, sched, stream);
+  if (d <= 16) return launch_exec_d<16>(p, topo, ops, sched, stream);
+  if (d <= 32) return launch_exec_d<32>(p, topo, ops, sched, stream);
+  if (d <= 64) return launch_exec_d<64>(p, topo, ops, sched, stream);
+  return launch_exec_d<128>(p, topo, ops, sched, stream);
 }
 
 int launch_checksums(const SumParams& p, void* stream) {
