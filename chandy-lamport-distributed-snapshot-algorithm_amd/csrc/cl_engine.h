@@ -88,14 +88,17 @@ struct Layout {
   // private column (words)
   int32_t w_fifo, w_chw, w_cur, w_int, w_pend, w_trig, priv;
   // shared region (words, after the 64 private columns)
-  int32_t x_pick, x_tslot, x_off, x_done, x_ndone, x_acc, shared;
+  int32_t x_pick, x_tslot, x_off, x_done, x_ndone, x_acc;
+  int32_t x_delay_begin;  // words of the shared region zeroed at start (everything before x_delay)
+  int32_t x_delay;        // wave's delay rows staged in LDS (0 = not staged; rows read from HBM)
+  int32_t shared;
   int32_t wave_words;
   // state image per instance (words): per node priv + G_NUM, then s_cap done counters + ndone
   int32_t state_words;
 };
 
 inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_log2, int32_t ocap_log2,
-                          int32_t s_cap) {
+                          int32_t s_cap, int64_t sched_row = 0, int32_t delay_budget_words = 0) {
   Layout L;
   L.cap_log2 = cap_log2;
   L.ocap_log2 = ocap_log2;
@@ -118,7 +121,15 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
   L.x_done = base + 3 * kWave;
   L.x_ndone = L.x_done + L.ipw * s_cap;
   L.x_acc = L.x_ndone + L.ipw;
-  L.shared = L.x_acc + 5 * L.ipw - base;
+  L.x_delay_begin = L.x_acc + 5 * L.ipw - base;
+  const int64_t delay_words = (int64_t)L.ipw * sched_row / 4;  // sched_row is a multiple of 16
+  if (sched_row > 0 && delay_words <= delay_budget_words) {
+    L.x_delay = (L.x_acc + 5 * L.ipw + 3) / 4 * 4;  // 16-byte aligned
+    L.shared = L.x_delay + (int32_t)delay_words - base;
+  } else {
+    L.x_delay = 0;
+    L.shared = L.x_delay_begin;
+  }
   L.wave_words = (base + L.shared + 3) / 4 * 4;
   L.state_words = n_nodes * (L.priv + G_NUM) + s_cap + 1;
   return L;
@@ -130,17 +141,20 @@ struct ExecParams {
   int32_t n_nodes, n_ch;
   Layout lay;
   int32_t n_started_before;  // snapshots started by ops before op_begin
+  int32_t topo_w;            // words per node block of the topology image (3 + max in-degree)
   // delays: draw k of an instance is sched[inst * sched_row + k], k < draws
   int64_t draws, sched_row;
   int64_t n_inst, stride;
-  int32_t fresh;
-  // state / outputs (instance-fastest, [k][stride])
-  uint32_t* state;     // [state_words]
-  int32_t* regs;       // [R_NUM]
-  int32_t* fin_tok;    // [N] final node tokens
-  int32_t* snap_tok;   // [S_cap][N]
-  uint32_t* snap_rec;  // [S_cap][C]  lo16 = begin, hi16 = end (channel token cursor)
-  int32_t* snap_tick;  // [S_cap]
+  int32_t fresh;       // start from the initial topology state (else resume from `state`)
+  int32_t save_state;  // write the resumable state image at the end
+  // state: [state_words][stride]; regs: [R_NUM][stride]
+  uint32_t* state;
+  int32_t* regs;
+  // outputs, node/channel index fastest so a wave's stores coalesce:
+  int32_t* fin_tok;    // [stride][N]          final node tokens
+  int32_t* snap_tok;   // [S_cap][stride][N]   tokenMap
+  uint32_t* snap_rec;  // [S_cap][stride][C]   lo16 = begin, hi16 = end (channel token cursor)
+  int32_t* snap_tick;  // [S_cap][stride]      completion tick or -1
   uint32_t* ovf;       // [C][1 << ocap_log2] spill ring
   uint32_t* ovh;       // [C] spill ring head
 };
@@ -160,9 +174,9 @@ struct SumParams {
 };
 
 // Topology image (uint32, uniform per node, read once per lane at kernel start):
-//   node v block at v * (3 + id): [indeg, outdeg, out_off, in[0..id)]
+//   node v block at v * topo_w (topo_w = 3 + max in-degree): [indeg, outdeg, out_off, in[0..indeg)]
 //     in[k] = src rank (bits 7..0) | sender's out-index of this channel (15..8) | channel id (31..16)
-//   then init_tok[N] at N * (3 + id)
+//   then init_tok[N] at N * topo_w
 // Launchers (cl_kernels.hip); return hipError_t as int.
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream);
 int launch_checksums(const SumParams& p, void* stream);

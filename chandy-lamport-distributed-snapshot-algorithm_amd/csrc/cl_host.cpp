@@ -29,6 +29,10 @@
 
 using namespace clsnap;
 
+// Per-wave LDS words available for staging the wave's delay rows (kernel reads the
+// delays from LDS instead of HBM when ipw * row fits).
+constexpr int32_t kDelayStageWords = 2048;
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -269,6 +273,8 @@ struct cl_sim {
   Layout lay{};
   int32_t s_cap = 0;
   bool need_fresh = true;
+  bool state_valid = false;  // the device state image matches ops[0, executed)
+  int64_t layout_row = 0;    // delay row length the LDS layout was sized for
   DevBuf<Op> d_ops;
   size_t ops_uploaded = 0;
   DevBuf<uint32_t> d_topo;
@@ -445,15 +451,25 @@ struct cl_sim {
     const int n = (int)ids.size(), C = (int)ch_dst.size();
     int32_t want_s = std::max<int32_t>(4, (n_sids + 3) / 4 * 4);
     int ocap = ocap_log2_needed();
-    if (!need_fresh && lay.wave_words && want_s <= s_cap && ocap <= lay.ocap_log2 && lay.cap_log2 == cap_log2)
+    if (!need_fresh && lay.wave_words && want_s <= s_cap && ocap <= lay.ocap_log2 && lay.cap_log2 == cap_log2 &&
+        layout_row == (go_seeds ? std::max<int64_t>(16, (draws_needed() + 15) / 16 * 16) : (user_draws + 15) / 16 * 16))
       return CL_OK;
     s_cap = std::max(want_s, s_cap);
     if (s_cap > kMaxSnapshots) return set_err(CL_E_LIMIT, "more than %d snapshots", kMaxSnapshots);
     if (n == 0) return set_err(CL_E_STATE, "the topology has no nodes");
-    Layout L = make_layout(n, max_out, max_in, cap_log2, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), s_cap);
+    int32_t dmax = 1;  // kernel degree bound (power of two); per-lane arrays are sized by it
+    while (dmax < std::max(max_out, max_in)) dmax *= 2;
+    const int64_t row = go_seeds ? std::max<int64_t>(16, (draws_needed() + 15) / 16 * 16) : (user_draws + 15) / 16 * 16;
+    Layout L = make_layout(n, dmax, dmax, cap_log2, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), s_cap,
+                           row, kDelayStageWords);
+    if (L.od < max_out || L.id < max_in) return set_err(CL_E_LIMIT, "layout does not cover the node degrees");
+    if ((uint64_t)s_cap * stride * (uint64_t)std::max(n, std::max(C, 1)) >= (1ull << 32) ||
+        (uint64_t)L.state_words * stride >= (1ull << 32))
+      return set_err(CL_E_LIMIT, "batch too large for 32-bit output indexing; split it");
     if ((int64_t)L.wave_words * kWavesPerBlock * 4 > kMaxLdsBytes)
       return set_err(CL_E_LIMIT, "per-wave state of %d words exceeds LDS (lower fifo slots or degree)", L.wave_words);
     lay = L;
+    layout_row = row;
     int rc;
     if ((rc = d_state.ensure((size_t)lay.state_words * stride))) return rc;
     if ((rc = d_regs.ensure((size_t)R_NUM * stride))) return rc;
@@ -491,6 +507,7 @@ struct cl_sim {
     p.n_ch = C;
     p.lay = lay;
     p.n_started_before = n_started_before;
+    p.topo_w = 3 + max_in;  // ensure_layout guarantees lay.od == lay.id >= every node's degree
     p.draws = dev_draws;
     p.sched_row = dev_row;
     p.n_inst = n_inst;
@@ -508,7 +525,7 @@ struct cl_sim {
   }
 
   // Launch pending ops (all ops when a fresh replay is needed). Asynchronous.
-  int launch(bool force_fresh) {
+  int launch(bool force_fresh, bool save_state) {
     int rc = freeze();
     if (rc) return rc;
     if ((rc = ensure_device())) return rc;
@@ -516,7 +533,10 @@ struct cl_sim {
     if (!d_topo.p && (rc = upload_topology())) return rc;
     if ((rc = ensure_layout())) return rc;
     if ((rc = ensure_delays())) return rc;
-    if (force_fresh) need_fresh = true;
+    if (lay.x_delay && dev_row != layout_row)
+      return set_err(CL_E_STATE, "delay rows (%lld) differ from the staged layout (%lld)", (long long)dev_row,
+                     (long long)layout_row);
+    if (force_fresh || !state_valid) need_fresh = true;
     if (!need_fresh && executed == (int32_t)ops.size()) return CL_OK;
     if (ops.size() > ops_uploaded || !d_ops.p) {
       if ((rc = d_ops.ensure(std::max<size_t>(ops.size(), 64)))) return rc;
@@ -531,6 +551,7 @@ struct cl_sim {
       if (lay.ocap_log2 >= 0) HIP_TRY(hipMemsetAsync(d_ovh.p, 0, d_ovh.n * sizeof(uint32_t), stream));
     }
     ExecParams p = exec_params(begin, started_before);
+    p.save_state = save_state ? 1 : 0;
     if (ev_used == 256 && (rc = fold_events())) return rc;
     if (ev_used == ev_pool.size()) {
       std::pair<hipEvent_t, hipEvent_t> pr;
@@ -548,6 +569,7 @@ struct cl_sim {
     timed = true;
     executed = (int32_t)ops.size();
     need_fresh = false;
+    state_valid = save_state;  // a rerun leaves no resumable image: the next flush replays
     h_valid = false;
     return CL_OK;
   }
@@ -561,7 +583,7 @@ struct cl_sim {
 
   int flush() {
     if (!frozen || executed != (int32_t)ops.size() || need_fresh) {
-      int rc = launch(false);
+      int rc = launch(false, true);
       if (rc) return rc;
     }
     return sync();
@@ -843,7 +865,7 @@ int cl_flush(cl_sim* sim) {
 
 int cl_rerun(cl_sim* sim) {
   SIM_CHECK(sim);
-  return sim->launch(true);
+  return sim->launch(true, false);
 }
 
 int cl_synchronize(cl_sim* sim) {
@@ -960,7 +982,8 @@ int cl_node_tokens(cl_sim* sim, int64_t inst, int64_t* out) {
   if (inst < 0 || inst >= sim->n_inst) return set_err(CL_E_INVALID, "instance out of range");
   int rc = sim->fetch();
   if (rc) return rc;
-  for (size_t r = 0; r < sim->ids.size(); ++r) out[r] = sim->h_tok[r * sim->stride + inst];
+  const size_t n = sim->ids.size();
+  for (size_t r = 0; r < n; ++r) out[r] = sim->h_tok[(size_t)inst * n + r];
   return CL_OK;
 }
 
@@ -985,12 +1008,12 @@ int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens,
   if (sim->h_snap_tick[(size_t)sid * st + inst] < 0)
     return set_err(CL_E_NOT_COMPLETE, "snapshot %d has not completed in instance %lld", sid, (long long)inst);
   const int n = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
-  for (int v = 0; v < n; ++v) tokens[v] = sim->h_snap_tok[((size_t)sid * n + v) * st + inst];
+  for (int v = 0; v < n; ++v) tokens[v] = sim->h_snap_tok[((size_t)sid * st + inst) * n + v];
   int64_t m = 0;
   bool fits = true;
   for (int c = 0; c < C; ++c) {
     msg_offsets[c] = m;
-    const uint32_t rec = sim->h_snap_rec[((size_t)sid * C + c) * st + inst];
+    const uint32_t rec = sim->h_snap_rec[((size_t)sid * st + inst) * C + c];
     const uint32_t b = rec & 0xffffu, e = rec >> 16;
     for (uint32_t k = b; k < e; ++k, ++m) {
       if (m < msg_cap) msg_tokens[m] = sim->hist[c][k];
@@ -1021,7 +1044,7 @@ int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out) {
     for (int32_t s = 0; s < sim->n_sids; ++s) {
       if (sim->h_snap_tick[(size_t)s * st + i] < 0) continue;
       for (int c = 0; c < C; ++c) {
-        const uint32_t rec = sim->h_snap_rec[((size_t)s * C + c) * st + i];
+        const uint32_t rec = sim->h_snap_rec[((size_t)s * st + i) * C + c];
         out[CL_CNT_RECORDED] += (rec >> 16) - (rec & 0xffffu);
       }
     }

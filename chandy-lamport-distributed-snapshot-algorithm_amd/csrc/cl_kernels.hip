@@ -35,17 +35,24 @@
 namespace clsnap {
 namespace {
 
+// LDS pointers carry their address space explicitly: a generic pointer lets the compiler
+// merge an LDS store with a global one into a FLAT store, and every FLAT op forces
+// s_waitcnt vmcnt(0) lgkmcnt(0) -- a full memory drain inside the tick loop.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
 // Uniform-per-lane context.  Output arrays are addressed with 32-bit element indices
 // (the host keeps every array below 2^32 elements).
 struct Ctx {
   const ExecParams& p;
   const Layout& lay;
-  uint32_t* P;  // this lane's private column: word k at P[k * 64]
-  uint32_t* X;  // this wave's LDS base (shared region at lay.x_*)
-  const uint8_t* __restrict__ row;  // this instance's delay row
+  lds_u32* P;  // this lane's private column: word k at P[k * 64]
+  lds_u32* X;  // this wave's LDS base (shared region at lay.x_*)
+  const uint8_t* __restrict__ row;  // this instance's delay row in HBM
+  const lds_u8* lrow;               // the same row staged in LDS (nullptr: read HBM)
   int32_t lane, seg_base, v, seg;
   uint32_t inst;      // instance index (0 for lanes without an instance)
-  uint32_t stride;    // instance stride of every [k][stride] array
+  uint32_t stride;    // padded instance count
   uint64_t seg_mask;  // the instance's lanes
   int32_t indeg, outdeg, out_off;
 };
@@ -61,6 +68,11 @@ struct Lane {
 
 #define PW(k) (x.P[(uint32_t)(k) << 6])
 #define XW(k) (x.X[(uint32_t)(k)])
+
+// LDS atomic add (ds_add_rtn_u32); the wave's lanes are the only users of these words.
+__device__ __forceinline__ uint32_t lds_add(lds_u32* a, uint32_t v) {
+  return __atomic_fetch_add(a, v, __ATOMIC_RELAXED);
+}
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -87,10 +99,10 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
   const uint32_t chw = PW(lay.w_chw + ko);
   const uint32_t cnt = (chw >> 8) & 0xffu;
   if (cnt >= (uint32_t)kMaxQueued) { ln.flag = ST_FIFO_OVERFLOW; return; }
-  const uint32_t delay = x.row[k];
+  const uint32_t delay = x.lrow ? x.lrow[k] : x.row[k];
   const uint32_t e = payload | ((uint32_t)(ln.time + 1 + (int32_t)delay) << 16);
   const uint32_t cap = 1u << lay.cap_log2;
-  if (cnt < cap) {
+  if (__builtin_expect(cnt < cap, 1)) {
     PW(lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + ((chw + cnt) & (cap - 1))) = e;
   } else {  // LDS ring full: younger packets of this channel spill to an HBM ring
     if (lay.ocap_log2 < 0 || cnt - cap >= (1u << lay.ocap_log2)) { ln.flag = ST_FIFO_OVERFLOW; return; }
@@ -107,39 +119,37 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
 // the one the first marker arrived on (arrive = -1 at the initiator).  A channel's
 // recording is the cursor interval [begin, end) over the tokens delivered on it.
 template <int D>
-__device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, int32_t sid, int32_t arrive) {
+__device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const uint32_t (&it)[D], int32_t sid,
+                                             int32_t arrive) {
   const ExecParams& p = x.p;
   const Layout& lay = x.lay;
-  p.snap_tok[((uint32_t)sid * p.n_nodes + x.v) * x.stride + x.inst] = ln.tokens;
+  const uint32_t r = (uint32_t)sid * x.stride + x.inst;
+  p.snap_tok[r * p.n_nodes + x.v] = ln.tokens;
+  uint32_t* rec = p.snap_rec + r * p.n_ch;
 #pragma unroll
   for (int32_t kj = 0; kj < D; ++kj) {
     if (kj < x.indeg) {
       const uint32_t cur = PW(lay.w_cur + kj);
-      const uint32_t cc = PW(lay.w_int + kj) >> 16;
-      p.snap_rec[((uint32_t)sid * p.n_ch + cc) * x.stride + x.inst] = kj == arrive ? (cur | (cur << 16)) : cur;
+      rec[it[kj] >> 16] = kj == arrive ? (cur | (cur << 16)) : cur;
     }
   }
-}
-
-__device__ __forceinline__ void set_pend(const Ctx& x, int32_t sid, uint32_t val) {
-  const uint32_t pi = x.lay.w_pend + (sid >> 2), sh = (sid & 3) * 8;
-  PW(pi) = (PW(pi) & ~(0xffu << sh)) | (val << sh);
 }
 
 // NotifyCompletedSnapshot (sim.go:126-131): the instance's snapshot completes when all N
 // nodes have; one LDS counter per (instance, snapshot).
 __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
-  const uint32_t old = atomicAdd(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
+  const uint32_t old = lds_add(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
   if (old + 1 == (uint32_t)x.p.n_nodes) {
     x.p.snap_tick[(uint32_t)sid * x.stride + x.inst] = ln.time;
-    atomicAdd(&XW(x.lay.x_ndone + x.seg), 1u);
+    lds_add(&XW(x.lay.x_ndone + x.seg), 1u);
   }
 }
 
 // Fold lane-local engine failures into the instance status (all lanes must call).
 __device__ __forceinline__ void resolve_failures(const Ctx& x, Lane& ln) {
-  if (__builtin_expect(__ballot(ln.flag != 0) == 0, 1)) return;
-  const uint64_t m = __ballot(ln.flag != 0) & x.seg_mask;
+  const uint64_t any = __ballot(ln.flag != 0);
+  if (__builtin_expect(any == 0, 1)) return;
+  const uint64_t m = any & x.seg_mask;
   const int32_t src = m ? (int32_t)__builtin_ctzll(m) : x.lane;
   const int32_t code = __shfl(ln.flag, src);
   if (m && ln.alive) {
@@ -149,121 +159,133 @@ __device__ __forceinline__ void resolve_failures(const Ctx& x, Lane& ln) {
   ln.flag = 0;
 }
 
-// Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
-// Must be reached by all lanes of the wave.  D bounds every node's in/out degree.
+// HandleMarker (node.go:149-171) for snapshot `sid` arriving on in-link ki from `src`.
 template <int D>
-__device__ __forceinline__ void tick(const Ctx& x, Lane& ln, bool act) {
+__device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const uint32_t (&it)[D], int32_t ki,
+                                              uint32_t src, int32_t sid, int32_t& ntrig) {
+  const Layout& lay = x.lay;
+  const uint32_t pi = lay.w_pend + (sid >> 2), sh = (sid & 3) * 8;
+  const uint32_t pw = PW(pi);
+  uint32_t pend;
+  if (!((ln.started >> sid) & 1u)) {  // first marker: record, then broadcast (phase D)
+    ln.started |= 1u << sid;
+    create_local<D>(x, ln, it, sid, ki);
+    pend = (uint32_t)x.indeg - 1;
+    if (x.outdeg) {
+      XW(lay.x_tslot + x.seg_base + src) = (uint32_t)x.outdeg;
+      PW(lay.w_trig + ntrig) = src | ((uint32_t)sid << 8);
+      ntrig++;
+    }
+  } else {  // later marker: stop recording this channel
+    const uint32_t r = (uint32_t)sid * x.stride + x.inst;
+    reinterpret_cast<uint16_t*>(x.p.snap_rec)[2 * (r * x.p.n_ch + (it[ki] >> 16)) + 1] =
+        (uint16_t)PW(lay.w_cur + ki);
+    pend = ((pw >> sh) & 0xffu) - 1;
+  }
+  PW(pi) = (pw & ~(0xffu << sh)) | (pend << sh);
+  if (pend == 0) node_complete(x, ln, sid);
+}
+
+// Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
+// Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
+// it[] holds this node's in-link words.
+template <int D>
+__device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const uint32_t (&it)[D], bool act) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
+  ln.time += act ? 1 : 0;
   // ---- A: pick ------------------------------------------------------------
   uint32_t pick = 0, empty_scanned = 0;
-  if (act) {
-    ln.time++;
-    bool done = false;
+  bool scanning = act;
 #pragma unroll
-    for (int32_t ko = 0; ko < D; ++ko) {
-      if (done || ko >= x.outdeg) continue;
-      const uint32_t chw = PW(lay.w_chw + ko);
-      const uint32_t cnt = (chw >> 8) & 0xffu;
-      if (!cnt) {
-        empty_scanned |= 1u << ko;
-        continue;
-      }
-      ln.peek++;
-      const uint32_t head = chw & 0xffu;
-      const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
-      const uint32_t e = PW(slot);
-      if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) continue;
-      if (cnt > cap) {  // refill the freed slot (the new tail) from the HBM spill ring
-        const uint32_t c = (uint32_t)(x.out_off + ko);
-        const uint32_t om = (1u << lay.ocap_log2) - 1;
-        uint32_t* hp = &x.p.ovh[c * x.stride + x.inst];
-        const uint32_t h = *hp;
-        PW(slot) = x.p.ovf[((c << lay.ocap_log2) + h) * x.stride + x.inst];
-        *hp = (h + 1) & om;
-      }
-      PW(lay.w_chw + ko) = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
-      pick = (e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16);
-      done = true;
+  for (int32_t ko = 0; ko < D; ++ko) {
+    const bool look = scanning && ko < x.outdeg;
+    const uint32_t chw = PW(lay.w_chw + ko);
+    const uint32_t cnt = (chw >> 8) & 0xffu;
+    const uint32_t head = chw & (cap - 1);
+    const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
+    const uint32_t e = PW(slot);
+    empty_scanned |= (look && cnt == 0) ? (1u << ko) : 0u;
+    const bool nonempty = look && cnt != 0;
+    ln.peek += nonempty ? 1u : 0u;
+    const bool due = nonempty && (int32_t)((e >> 16) & 0x7fffu) <= ln.time;
+    if (__builtin_expect(due && cnt > cap, 0)) {  // refill the freed slot from the HBM spill ring
+      const uint32_t c = (uint32_t)(x.out_off + ko);
+      const uint32_t om = (1u << lay.ocap_log2) - 1;
+      uint32_t* hp = &x.p.ovh[c * x.stride + x.inst];
+      const uint32_t h = *hp;
+      PW(slot) = x.p.ovf[((c << lay.ocap_log2) + h) * x.stride + x.inst];
+      *hp = (h + 1) & om;
     }
+    const uint32_t popped = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
+    PW(lay.w_chw + ko) = due ? popped : chw;
+    pick = due ? ((e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16)) : pick;
+    scanning = scanning && !due;
   }
   XW(lay.x_pick + x.lane) = pick;
   wave_sync();
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
-  if (act) {
 #pragma unroll
-    for (int32_t ki = 0; ki < D; ++ki) {
-      if (ki >= x.indeg) continue;
-      const uint32_t it = PW(lay.w_int + ki);
-      const uint32_t src = it & 0xffu;
-      const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
-      if (!(pk & kPickValid) || ((pk >> 16) & 0x7fu) != ((it >> 8) & 0xffu)) continue;
-      const uint32_t pay = pk & 0xffffu;
-      if (!(pk & kMarkerBit)) {  // HandleToken: tokens += data; recording cursor advances
-        ln.pop_tok++;
-        ln.tokens += (int32_t)pay;
-        PW(lay.w_cur + ki) += 1u;
-        continue;
-      }
-      ln.pop_mk++;  // HandleMarker
-      const int32_t sid = (int32_t)pay;
-      const uint32_t sh = (sid & 3) * 8;
-      uint32_t pend;
-      if (!((ln.started >> sid) & 1u)) {
-        ln.started |= 1u << sid;
-        create_local<D>(x, ln, sid, ki);
-        pend = (uint32_t)x.indeg - 1;
-        if (x.outdeg) {
-          XW(lay.x_tslot + x.seg_base + src) = (uint32_t)x.outdeg;
-          PW(lay.w_trig + ntrig) = src | ((uint32_t)sid << 8);
-          ntrig++;
-        }
-      } else {
-        reinterpret_cast<uint16_t*>(x.p.snap_rec)[2 * (((uint32_t)sid * x.p.n_ch + (it >> 16)) * x.stride + x.inst) + 1] =
-            (uint16_t)PW(lay.w_cur + ki);
-        pend = ((PW(lay.w_pend + (sid >> 2)) >> sh) & 0xffu) - 1;
-      }
-      set_pend(x, sid, pend);
-      if (pend == 0) node_complete(x, ln, sid);
-    }
+  for (int32_t ki = 0; ki < D; ++ki) {
+    const uint32_t src = it[ki] & 0xffu;
+    const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
+    const bool m = act && ki < x.indeg && (pk & kPickValid) && ((pk >> 16) & 0x7fu) == ((it[ki] >> 8) & 0xffu);
+    const bool mk = m && (pk & kMarkerBit);
+    const bool tok = m && !mk;
+    const uint32_t pay = pk & 0xffffu;
+    // HandleToken: tokens += data; the channel's recording cursor advances
+    ln.tokens += tok ? (int32_t)pay : 0;
+    ln.pop_tok += tok ? 1u : 0u;
+    ln.pop_mk += mk ? 1u : 0u;
+    const uint32_t cur = PW(lay.w_cur + ki);
+    PW(lay.w_cur + ki) = cur + (tok ? 1u : 0u);
+    if (mk) handle_marker<D>(x, ln, it, ki, src, (int32_t)pay, ntrig);
   }
   // ---- C/D: broadcast draws in sender order, then push -------------------------
   if (__ballot(ntrig > 0)) {
     wave_sync();
     const uint32_t t = XW(lay.x_tslot + x.lane);
     XW(lay.x_tslot + x.lane) = 0;
-    const uint32_t incl = wave_incl_scan(t);
-    XW(lay.x_off + x.lane) = incl;
+    XW(lay.x_off + x.lane) = wave_incl_scan(t);
     wave_sync();
     const uint32_t base = x.seg_base > 0 ? XW(lay.x_off + x.seg_base - 1) : 0u;
-    if (act) {
-      for (int32_t kk = 0; kk < ntrig; ++kk) {
-        const uint32_t tv = PW(lay.w_trig + kk);
-        const uint32_t src = tv & 0xffu;
-        const uint32_t sid = tv >> 8;
-        // exclusive prefix of the triggering sender within the instance
-        const int64_t k0 = (int64_t)ln.draw + (XW(lay.x_off + x.seg_base + src) - (uint32_t)x.outdeg - base);
+    const uint32_t total = XW(lay.x_off + x.seg_base + x.p.n_nodes - 1) - base;
+    for (int32_t kk = 0; kk < ntrig; ++kk) {
+      const uint32_t tv = PW(lay.w_trig + kk);
+      const uint32_t src = tv & 0xffu;
+      const uint32_t sid = tv >> 8;
+      // exclusive prefix of the triggering sender within the instance
+      const int64_t k0 = (int64_t)ln.draw + (XW(lay.x_off + x.seg_base + src) - (uint32_t)x.outdeg - base);
 #pragma unroll
-        for (int32_t j = 0; j < D; ++j) {
-          if (j >= x.outdeg) continue;
-          push(x, ln, j, kMarkerBit | sid, k0 + j);
-          // the reference scans this sender's links after the push when the trigger came
-          // from a lower rank: a link that was empty at tick start gets peeked once more
-          if ((int32_t)src < x.v && ((empty_scanned >> j) & 1u)) {
-            ln.peek++;
-            empty_scanned &= ~(1u << j);
-          }
+      for (int32_t j = 0; j < D; ++j) {
+        if (j >= x.outdeg) continue;
+        push(x, ln, j, kMarkerBit | sid, k0 + j);
+        // the reference scans this sender's links after the push when the trigger came
+        // from a lower rank: a link that was empty at tick start gets peeked once more
+        if ((int32_t)src < x.v && ((empty_scanned >> j) & 1u)) {
+          ln.peek++;
+          empty_scanned &= ~(1u << j);
         }
       }
-      ln.draw += (int32_t)(XW(lay.x_off + x.seg_base + x.p.n_nodes - 1) - base);
     }
+    ln.draw += act ? (int32_t)total : 0;
   }
   resolve_failures(x, ln);
 }
 
+// Occupancy target per degree bound (waves per SIMD; 256-thread workgroups).  Forcing
+// 8 waves/SIMD at D = 1 costs scratch spills; CLSNAP_OCC selects the policy (0 = let the
+// compiler choose, 1 = force the targets) -- an A/B knob, see DESIGN.md §9.
+#ifndef CLSNAP_OCC
+#define CLSNAP_OCC 0
+#endif
+constexpr int waves_for(int D) {
+  return CLSNAP_OCC ? (D <= 2 ? 8 : D <= 4 ? 6 : D <= 8 ? 4 : 2) : 1;
+}
+
 template <int D>
-__global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
+__global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
                                                                          const Op* __restrict__ ops,
                                                                          const uint8_t* __restrict__ sched) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -272,26 +294,39 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
   const int32_t lane = threadIdx.x & (kWave - 1);
   const int32_t wib = threadIdx.x / kWave;
   const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
-  uint32_t* X = lds + (size_t)wib * lay.wave_words;
+  lds_u32* X = (lds_u32*)(lds + (size_t)wib * lay.wave_words);
   const int32_t seg = lane / N;
   const int32_t v = lane - seg * N;
   const uint32_t inst = wave * (uint32_t)lay.ipw + seg;
   const bool valid = seg < lay.ipw && inst < p.n_inst;
   const uint32_t ii = valid ? inst : 0u;  // safe index for lanes without an instance
-  const uint32_t* nb = topo + (size_t)v * (3 + lay.id);
+  const uint32_t* nb = topo + (size_t)(valid ? v : 0) * p.topo_w;
   const int32_t indeg = valid ? (int32_t)nb[0] : 0;
   const int32_t outdeg = valid ? (int32_t)nb[1] : 0;
   const uint64_t seg_mask = N == 64 ? ~0ull : (((1ull << N) - 1) << (seg * N));
   const uint32_t st = (uint32_t)p.stride;
-  const Ctx x{p, lay, X + lane, X, sched + (size_t)ii * p.sched_row, lane, seg * N, v, seg, ii, st, seg_mask,
+  // Stage the wave's delay rows (ipw contiguous rows of sched_row bytes) in LDS when they fit.
+  const bool staged = lay.x_delay > 0;
+  const lds_u8* lrow = staged ? (const lds_u8*)(X + lay.x_delay) + (size_t)seg * p.sched_row : nullptr;
+  if (staged) {
+    const uint32_t first = wave * (uint32_t)lay.ipw;
+    const uint32_t nrow = min((uint32_t)lay.ipw, (uint32_t)p.n_inst - min(first, (uint32_t)p.n_inst));
+    const uint32_t words = nrow * (uint32_t)(p.sched_row / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)first * p.sched_row);
+    for (uint32_t k = lane; k < words; k += kWave) X[lay.x_delay + k] = src[k];
+  }
+  const Ctx x{p, lay, X + lane, X, sched + (size_t)ii * p.sched_row, lrow, lane, seg * N, v, seg, ii, st, seg_mask,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0};
+  uint32_t it[D];
+#pragma unroll
+  for (int32_t k = 0; k < D; ++k) it[k] = k < indeg ? nb[3 + k] : 0u;
 
   Lane ln;
   ln.flag = 0;
-  for (int32_t k = lane; k < lay.shared; k += kWave) XW(lay.priv * kWave + k) = 0u;
+  for (int32_t k = lane; k < lay.x_delay_begin; k += kWave) XW(lay.priv * kWave + k) = 0u;
   if (p.fresh) {
     for (int32_t k = 0; k < lay.priv; ++k) PW(k) = 0u;
-    ln.tokens = valid ? (int32_t)topo[(size_t)N * (3 + lay.id) + v] : 0;
+    ln.tokens = valid ? (int32_t)topo[(size_t)N * p.topo_w + v] : 0;
     ln.started = 0;
     ln.time = ln.draw = ln.status = 0;
     ln.peek = ln.pop_tok = ln.pop_mk = ln.push = 0;
@@ -316,7 +351,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
       XW(lay.x_ndone + seg) = Dn[lay.s_cap * st];
     }
   }
-  for (int32_t k = 0; k < indeg; ++k) PW(lay.w_int + k) = nb[3 + k];
   wave_sync();
   ln.alive = valid && ln.status == ST_OK;
   int32_t n_started = p.n_started_before;
@@ -325,19 +359,21 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
     const Op op = ops[i];
     if (op.kind == OP_SEND) {
       // SendTokens (node.go:112-131): balance check, link lookup, push -- all at src
-      int32_t f = 0;
-      if (ln.alive && v == op.a) {
-        if (ln.tokens < op.c) f = ST_FATAL_INSUFFICIENT;
-        else if (op.b < 0) f = ST_FATAL_UNKNOWN_DEST;
-        else {
-          ln.tokens -= op.c;
-          push(x, ln, op.b, (uint32_t)op.c, ln.draw);
-        }
+      const bool me = ln.alive && v == op.a;
+      const bool insufficient = me && ln.tokens < op.c;
+      const bool fatal = ((__ballot(insufficient) >> (x.seg_base + op.a)) & 1ull) != 0;
+      if (me && !insufficient && op.b >= 0) {
+        ln.tokens -= op.c;
+#pragma unroll
+        for (int32_t j = 0; j < D; ++j)  // static register indices for the out-link
+          if (j == op.b) push(x, ln, j, (uint32_t)op.c, ln.draw);
       }
-      const int32_t fs = __shfl(f, x.seg_base + op.a);
       if (ln.alive) {
-        if (fs) {
-          ln.status = fs;
+        if (fatal) {
+          ln.status = ST_FATAL_INSUFFICIENT;
+          ln.alive = false;
+        } else if (op.b < 0) {
+          ln.status = ST_FATAL_UNKNOWN_DEST;
           ln.alive = false;
         } else {
           ln.draw += 1;
@@ -348,8 +384,9 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
       // sim.StartSnapshot -> node.StartSnapshot: the initiator records every in-channel
       if (ln.alive && v == op.a) {
         ln.started |= 1u << op.b;
-        create_local<D>(x, ln, op.b, -1);
-        set_pend(x, op.b, (uint32_t)indeg);
+        create_local<D>(x, ln, it, op.b, -1);
+        const uint32_t pi = lay.w_pend + (op.b >> 2), sh = (op.b & 3) * 8;
+        PW(pi) = (PW(pi) & ~(0xffu << sh)) | ((uint32_t)indeg << sh);
 #pragma unroll
         for (int32_t j = 0; j < D; ++j)
           if (j < outdeg) push(x, ln, j, kMarkerBit | (uint32_t)op.b, (int64_t)ln.draw + j);
@@ -372,13 +409,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
         }
         const bool act = ln.alive && (waiting || rem > 0);
         if (!__ballot(act)) break;
-        tick<D>(x, ln, act);
-        if (act && !waiting) rem--;
+        tick<D>(x, ln, it, act);
+        rem -= (act && !waiting) ? 1 : 0;
       }
     }
   }
 
-  // ---- epilogue: tokens still queued, per-instance sums, state image -----------
+  // ---- epilogue: tokens still queued, per-instance sums, outputs, state image ------
   int32_t inflight = 0;
   {
     const uint32_t cap = 1u << lay.cap_log2;
@@ -401,16 +438,30 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
     }
   }
   if (valid) {
-    uint32_t* acc = &XW(lay.x_acc + 5 * seg);
-    atomicAdd(acc + 0, ln.peek);
-    atomicAdd(acc + 1, ln.pop_tok);
-    atomicAdd(acc + 2, ln.pop_mk);
-    atomicAdd(acc + 3, ln.push);
-    atomicAdd(acc + 4, (uint32_t)inflight);
+    lds_u32* acc = &XW(lay.x_acc + 5 * seg);
+    lds_add(acc + 0, ln.peek);
+    lds_add(acc + 1, ln.pop_tok);
+    lds_add(acc + 2, ln.pop_mk);
+    lds_add(acc + 3, ln.push);
+    lds_add(acc + 4, (uint32_t)inflight);
   }
   wave_sync();
   if (!valid) return;
-  p.fin_tok[(uint32_t)v * st + ii] = ln.tokens;
+  p.fin_tok[ii * (uint32_t)N + v] = ln.tokens;
+  if (v == 0) {
+    const lds_u32* acc = &XW(lay.x_acc + 5 * seg);
+    int32_t* r = p.regs + ii;
+    r[R_TIME * st] = ln.time;
+    r[R_DRAW * st] = ln.draw;
+    r[R_STATUS * st] = ln.status;
+    r[R_NDONE * st] = (int32_t)XW(lay.x_ndone + seg);
+    r[R_PEEK * st] = (int32_t)acc[0];
+    r[R_POP_TOK * st] = (int32_t)acc[1];
+    r[R_POP_MK * st] = (int32_t)acc[2];
+    r[R_PUSH * st] = (int32_t)acc[3];
+    r[R_INFLIGHT_TOK * st] = (int32_t)acc[4];
+  }
+  if (!p.save_state) return;
   uint32_t* S = p.state + ii;
   const uint32_t b = (uint32_t)v * (lay.priv + G_NUM);
   for (int32_t k = 0; k < lay.priv; ++k) S[(b + k) * st] = PW(k);
@@ -428,17 +479,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock) void cl_exec_kernel(ExecPar
     uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
     for (int32_t s = 0; s < lay.s_cap; ++s) Dn[s * st] = XW(lay.x_done + seg * lay.s_cap + s);
     Dn[lay.s_cap * st] = XW(lay.x_ndone + seg);
-    const uint32_t* acc = &XW(lay.x_acc + 5 * seg);
-    int32_t* r = p.regs + ii;
-    r[R_TIME * st] = ln.time;
-    r[R_DRAW * st] = ln.draw;
-    r[R_STATUS * st] = ln.status;
-    r[R_NDONE * st] = (int32_t)XW(lay.x_ndone + seg);
-    r[R_PEEK * st] = (int32_t)acc[0];
-    r[R_POP_TOK * st] = (int32_t)acc[1];
-    r[R_POP_MK * st] = (int32_t)acc[2];
-    r[R_PUSH * st] = (int32_t)acc[3];
-    r[R_INFLIGHT_TOK * st] = (int32_t)acc[4];
   }
 }
 
@@ -467,12 +507,12 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
       uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)sid;
       int64_t total = 0;
       for (int32_t n = 0; n < p.n_nodes; ++n) {
-        const int32_t t = p.snap_tok[((int64_t)sid * p.n_nodes + n) * p.stride + inst];
+        const int32_t t = p.snap_tok[((int64_t)sid * p.stride + inst) * p.n_nodes + n];
         h = mix64(h ^ (uint64_t)(int64_t)t);
         total += t;
       }
       for (int32_t c = 0; c < p.n_ch; ++c) {
-        const uint32_t rec = p.snap_rec[((int64_t)sid * p.n_ch + c) * p.stride + inst];
+        const uint32_t rec = p.snap_rec[((int64_t)sid * p.stride + inst) * p.n_ch + c];
         const uint32_t b = rec & 0xffffu, e = rec >> 16;
         h = mix64(h ^ ((uint64_t)c << 32) ^ (uint64_t)(e - b));
         const int32_t* hv = p.hist_val + p.hist_off[c];
@@ -489,7 +529,7 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
     v[6] = cut;
     v[8] = (unsigned long long)ncomplete;
     int64_t fin = inflight;
-    for (int32_t n = 0; n < p.n_nodes; ++n) fin += p.fin_tok[(int64_t)n * p.stride + inst];
+    for (int32_t n = 0; n < p.n_nodes; ++n) fin += p.fin_tok[inst * p.n_nodes + n];
     const int64_t d = fin - p.total_tokens;
     v[7] = (unsigned long long)(d < 0 ? -d : d);
   }
@@ -516,7 +556,7 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
 
 // The kernel is instantiated for degree bounds 1, 2, 4, 8, 16, 32, 64, 128.
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
-  const int32_t d = p.lay.od > p.lay.id ? p.lay.od : p.lay.id;
+  const int32_t d = p.lay.od;  // the host sizes od == id == the power-of-two degree bound
   if (d <= 1) return launch_exec_d<1>(p, topo, ops, sched, stream);
   if (d <= 2) return launch_exec_d<2>(p, topo, ops, sched, stream);
   if (d <= 4) return launch_exec_d<4>(p, topo, ops, sched, stream);

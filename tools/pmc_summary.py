@@ -17,6 +17,6 @@ def summary(paths, kernel="cl_exec_kernel"):
 
 if __name__ == "__main__":
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    s = summary(glob.glob(f"{root}/pmc*/p_counter_collection.csv"))
+    s = summary(glob.glob(f"{root}/*/p_counter_collection.csv"))
     for k in sorted(s):
         print(f"{k:28s} {s[k]:16.1f}")
