@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--instances", type=int, default=0, help="instances per GPU (default: config)")
-    ap.add_argument("--fifo-slots", type=int, default=8)
+    ap.add_argument("--fifo-slots", type=int, default=0, help="LDS ring slots per channel (0 = automatic)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -184,7 +184,7 @@ class ChandyLamportSim:
         _check(self._L.cl_set_device(self._h, device))
         _check(self._L.cl_set_delay_go_seeds(self._h, seed_base))
         if fifo_lds_slots is not None or max_drain_ticks is not None:
-            _check(self._L.cl_set_limits(self._h, fifo_lds_slots or 8,
+            _check(self._L.cl_set_limits(self._h, fifo_lds_slots or 0,
                                          10000 if max_drain_ticks is None else max_drain_ticks))
 
     def __del__(self):
@@ -268,7 +268,7 @@ class ChandyLamportSim:
     def set_delay_go_seeds(self, seed_base):
         _check(self._L.cl_set_delay_go_seeds(self._h, seed_base))
 
-    def set_limits(self, fifo_lds_slots=8, max_drain_ticks=10000):
+    def set_limits(self, fifo_lds_slots=0, max_drain_ticks=10000):
         _check(self._L.cl_set_limits(self._h, fifo_lds_slots, max_drain_ticks))
 
     def flush(self):

@@ -32,6 +32,8 @@ using namespace clsnap;
 // Per-wave LDS words available for staging the wave's delay rows (kernel reads the
 // delays from LDS instead of HBM when ipw * row fits).
 constexpr int32_t kDelayStageWords = 2048;
+// Workgroups (4 waves each) per CU the automatic FIFO sizing keeps LDS from limiting.
+constexpr int32_t kTargetBlocks = 4;
 
 namespace {
 
@@ -235,6 +237,7 @@ struct cl_sim {
 
   // limits
   int32_t cap_log2 = 3;
+  bool auto_cap = true;  // choose cap_log2 per layout (cl_set_limits with slots > 0 pins it)
   int64_t max_drain = 10000;
 
   // delays
@@ -457,12 +460,24 @@ struct cl_sim {
     s_cap = std::max(want_s, s_cap);
     if (s_cap > kMaxSnapshots) return set_err(CL_E_LIMIT, "more than %d snapshots", kMaxSnapshots);
     if (n == 0) return set_err(CL_E_STATE, "the topology has no nodes");
-    int32_t dmax = 1;  // kernel degree bound (power of two); per-lane arrays are sized by it
-    while (dmax < std::max(max_out, max_in)) dmax *= 2;
     const int64_t row = go_seeds ? std::max<int64_t>(16, (draws_needed() + 15) / 16 * 16) : (user_draws + 15) / 16 * 16;
-    Layout L = make_layout(n, dmax, dmax, cap_log2, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), s_cap,
+    const int32_t od = std::max(max_out, 1), id = std::max(max_in, 1);
+    if (auto_cap) {
+      // LDS ring slots per channel: enough for the deepest channel (spill beyond), but
+      // small enough that LDS does not cap the workgroups per CU below kTargetBlocks.
+      int32_t mx = 1;
+      for (auto d : depth_bound) mx = std::max(mx, d);
+      int l = 1;
+      while (l < 3 && (1 << l) < mx) ++l;  // at most 8 slots
+      for (; l > 1; --l) {
+        Layout t = make_layout(n, od, id, l, -1, s_cap, row, kDelayStageWords);
+        if ((int64_t)t.wave_words * kWavesPerBlock * 4 * kTargetBlocks <= kMaxLdsBytes) break;
+      }
+      cap_log2 = l;
+      ocap = ocap_log2_needed();
+    }
+    Layout L = make_layout(n, od, id, cap_log2, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), s_cap,
                            row, kDelayStageWords);
-    if (L.od < max_out || L.id < max_in) return set_err(CL_E_LIMIT, "layout does not cover the node degrees");
     if ((uint64_t)s_cap * stride * (uint64_t)std::max(n, std::max(C, 1)) >= (1ull << 32) ||
         (uint64_t)L.state_words * stride >= (1ull << 32))
       return set_err(CL_E_LIMIT, "batch too large for 32-bit output indexing; split it");
@@ -724,14 +739,20 @@ int cl_set_device(cl_sim* sim, int32_t device_ordinal) {
 
 int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks) {
   SIM_CHECK(sim);
+  if (max_drain_ticks < 0) return set_err(CL_E_INVALID, "max_drain_ticks must be >= 0");
+  sim->max_drain = max_drain_ticks;
+  if (fifo_lds_slots == 0) {  // automatic
+    if (!sim->auto_cap) sim->need_fresh = true;
+    sim->auto_cap = true;
+    return CL_OK;
+  }
   int l = 0;
   while ((1 << l) < fifo_lds_slots) ++l;
   if (fifo_lds_slots < 2 || fifo_lds_slots > 64 || (1 << l) != fifo_lds_slots)
-    return set_err(CL_E_INVALID, "fifo_lds_slots must be a power of two in [2, 64]");
-  if (max_drain_ticks < 0) return set_err(CL_E_INVALID, "max_drain_ticks must be >= 0");
-  if (l != sim->cap_log2) sim->need_fresh = true;
+    return set_err(CL_E_INVALID, "fifo_lds_slots must be 0 (automatic) or a power of two in [2, 64]");
+  if (l != sim->cap_log2 || sim->auto_cap) sim->need_fresh = true;
   sim->cap_log2 = l;
-  sim->max_drain = max_drain_ticks;
+  sim->auto_cap = false;
   return CL_OK;
 }
 

@@ -48,12 +48,11 @@ struct Ctx {
   const Layout& lay;
   lds_u32* P;  // this lane's private column: word k at P[k * 64]
   lds_u32* X;  // this wave's LDS base (shared region at lay.x_*)
-  const uint8_t* __restrict__ row;  // this instance's delay row in HBM
-  const lds_u8* lrow;               // the same row staged in LDS (nullptr: read HBM)
+  const uint8_t* __restrict__ sched;  // delay schedule in HBM (row inst * sched_row)
+  const lds_u8* lrow;                 // this instance's row staged in LDS (nullptr: read HBM)
   int32_t lane, seg_base, v, seg;
   uint32_t inst;      // instance index (0 for lanes without an instance)
   uint32_t stride;    // padded instance count
-  uint64_t seg_mask;  // the instance's lanes
   int32_t indeg, outdeg, out_off;
 };
 
@@ -65,6 +64,29 @@ struct Lane {
   bool alive;    // instance still running (uniform within the segment)
   int32_t flag;  // lane-local engine failure raised during an op/tick
 };
+
+// Small degree bounds keep loops unrolled and predicated with the in-link words in
+// registers; larger ones use compact runtime loops over the node's own degree with the
+// in-link words in the lane's LDS column (fewer VGPRs, one copy of the marker path).
+// Code-shape knobs (A/B-tested per degree bound):
+//   CLSNAP_UNROLL_MAX  largest D whose loops are unrolled with in-link words in registers
+//   CLSNAP_A_PRED      phase A (pick) as predicated straight-line code (1) or branches (0)
+//   CLSNAP_B_PRED      phase B (receive) likewise
+#ifndef CLSNAP_UNROLL_MAX
+#define CLSNAP_UNROLL_MAX 4
+#endif
+#ifndef CLSNAP_A_PRED
+#define CLSNAP_A_PRED 1
+#endif
+#ifndef CLSNAP_B_PRED
+#define CLSNAP_B_PRED 1
+#endif
+#ifndef CLSNAP_MAX_D
+#define CLSNAP_MAX_D 128
+#endif
+constexpr bool unrolled(int D) { return D <= CLSNAP_UNROLL_MAX; }
+template <int D>
+using InLinks = uint32_t[unrolled(D) ? D : 1];
 
 #define PW(k) (x.P[(uint32_t)(k) << 6])
 #define XW(k) (x.X[(uint32_t)(k)])
@@ -99,7 +121,7 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
   const uint32_t chw = PW(lay.w_chw + ko);
   const uint32_t cnt = (chw >> 8) & 0xffu;
   if (cnt >= (uint32_t)kMaxQueued) { ln.flag = ST_FIFO_OVERFLOW; return; }
-  const uint32_t delay = x.lrow ? x.lrow[k] : x.row[k];
+  const uint32_t delay = x.lrow ? x.lrow[k] : x.sched[(size_t)x.inst * x.p.sched_row + k];
   const uint32_t e = payload | ((uint32_t)(ln.time + 1 + (int32_t)delay) << 16);
   const uint32_t cap = 1u << lay.cap_log2;
   if (__builtin_expect(cnt < cap, 1)) {
@@ -119,18 +141,25 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
 // the one the first marker arrived on (arrive = -1 at the initiator).  A channel's
 // recording is the cursor interval [begin, end) over the tokens delivered on it.
 template <int D>
-__device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const uint32_t (&it)[D], int32_t sid,
+__device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLinks<D>& it, int32_t sid,
                                              int32_t arrive) {
   const ExecParams& p = x.p;
   const Layout& lay = x.lay;
   const uint32_t r = (uint32_t)sid * x.stride + x.inst;
   p.snap_tok[r * p.n_nodes + x.v] = ln.tokens;
   uint32_t* rec = p.snap_rec + r * p.n_ch;
+  if constexpr (unrolled(D)) {
 #pragma unroll
-  for (int32_t kj = 0; kj < D; ++kj) {
-    if (kj < x.indeg) {
+    for (int32_t kj = 0; kj < D; ++kj) {
+      if (kj < x.indeg) {
+        const uint32_t cur = PW(lay.w_cur + kj);
+        rec[it[kj] >> 16] = kj == arrive ? (cur | (cur << 16)) : cur;
+      }
+    }
+  } else {
+    for (int32_t kj = 0; kj < x.indeg; ++kj) {
       const uint32_t cur = PW(lay.w_cur + kj);
-      rec[it[kj] >> 16] = kj == arrive ? (cur | (cur << 16)) : cur;
+      rec[PW(lay.w_int + kj) >> 16] = kj == arrive ? (cur | (cur << 16)) : cur;
     }
   }
 }
@@ -149,7 +178,9 @@ __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t si
 __device__ __forceinline__ void resolve_failures(const Ctx& x, Lane& ln) {
   const uint64_t any = __ballot(ln.flag != 0);
   if (__builtin_expect(any == 0, 1)) return;
-  const uint64_t m = any & x.seg_mask;
+  const int32_t N = x.p.n_nodes;
+  const uint64_t seg_mask = N == 64 ? ~0ull : (((1ull << N) - 1) << x.seg_base);
+  const uint64_t m = any & seg_mask;
   const int32_t src = m ? (int32_t)__builtin_ctzll(m) : x.lane;
   const int32_t code = __shfl(ln.flag, src);
   if (m && ln.alive) {
@@ -159,9 +190,15 @@ __device__ __forceinline__ void resolve_failures(const Ctx& x, Lane& ln) {
   ln.flag = 0;
 }
 
+template <int D>
+__device__ __forceinline__ uint32_t in_word(const Ctx& x, const InLinks<D>& it, int32_t k) {
+  if constexpr (unrolled(D)) return it[k];
+  else return PW(x.lay.w_int + k);
+}
+
 // HandleMarker (node.go:149-171) for snapshot `sid` arriving on in-link ki from `src`.
 template <int D>
-__device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const uint32_t (&it)[D], int32_t ki,
+__device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLinks<D>& it, int32_t ki,
                                               uint32_t src, int32_t sid, int32_t& ntrig) {
   const Layout& lay = x.lay;
   const uint32_t pi = lay.w_pend + (sid >> 2), sh = (sid & 3) * 8;
@@ -178,7 +215,7 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const uint
     }
   } else {  // later marker: stop recording this channel
     const uint32_t r = (uint32_t)sid * x.stride + x.inst;
-    reinterpret_cast<uint16_t*>(x.p.snap_rec)[2 * (r * x.p.n_ch + (it[ki] >> 16)) + 1] =
+    reinterpret_cast<uint16_t*>(x.p.snap_rec)[2 * (r * x.p.n_ch + (in_word<D>(x, it, ki) >> 16)) + 1] =
         (uint16_t)PW(lay.w_cur + ki);
     pend = ((pw >> sh) & 0xffu) - 1;
   }
@@ -186,61 +223,113 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const uint
   if (pend == 0) node_complete(x, ln, sid);
 }
 
+// Pop from a channel whose younger packets spilled: refill the freed LDS slot (the ring's
+// new tail) with the oldest spilled packet.
+__device__ __forceinline__ void refill(const Ctx& x, int32_t ko, uint32_t slot) {
+  const Layout& lay = x.lay;
+  const uint32_t c = (uint32_t)(x.out_off + ko);
+  const uint32_t om = (1u << lay.ocap_log2) - 1;
+  uint32_t* hp = &x.p.ovh[c * x.stride + x.inst];
+  const uint32_t h = *hp;
+  PW(slot) = x.p.ovf[((c << lay.ocap_log2) + h) * x.stride + x.inst];
+  *hp = (h + 1) & om;
+}
+
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
 // Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
 // it[] holds this node's in-link words.
 template <int D>
-__device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const uint32_t (&it)[D], bool act) {
+__device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
   ln.time += act ? 1 : 0;
   // ---- A: pick ------------------------------------------------------------
   uint32_t pick = 0, empty_scanned = 0;
-  bool scanning = act;
+  if constexpr (unrolled(D) && CLSNAP_A_PRED) {
+    bool scanning = act;
 #pragma unroll
-  for (int32_t ko = 0; ko < D; ++ko) {
-    const bool look = scanning && ko < x.outdeg;
-    const uint32_t chw = PW(lay.w_chw + ko);
-    const uint32_t cnt = (chw >> 8) & 0xffu;
-    const uint32_t head = chw & (cap - 1);
-    const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
-    const uint32_t e = PW(slot);
-    empty_scanned |= (look && cnt == 0) ? (1u << ko) : 0u;
-    const bool nonempty = look && cnt != 0;
-    ln.peek += nonempty ? 1u : 0u;
-    const bool due = nonempty && (int32_t)((e >> 16) & 0x7fffu) <= ln.time;
-    if (__builtin_expect(due && cnt > cap, 0)) {  // refill the freed slot from the HBM spill ring
-      const uint32_t c = (uint32_t)(x.out_off + ko);
-      const uint32_t om = (1u << lay.ocap_log2) - 1;
-      uint32_t* hp = &x.p.ovh[c * x.stride + x.inst];
-      const uint32_t h = *hp;
-      PW(slot) = x.p.ovf[((c << lay.ocap_log2) + h) * x.stride + x.inst];
-      *hp = (h + 1) & om;
+    for (int32_t ko = 0; ko < D; ++ko) {
+      if (ko >= lay.od) break;  // uniform: the layout holds od out-links per lane
+      const bool look = scanning && ko < x.outdeg;
+      const uint32_t chw = PW(lay.w_chw + ko);
+      const uint32_t cnt = (chw >> 8) & 0xffu;
+      const uint32_t head = chw & (cap - 1);
+      const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
+      const uint32_t e = PW(slot);
+      empty_scanned |= (look && cnt == 0) ? (1u << ko) : 0u;
+      const bool nonempty = look && cnt != 0;
+      ln.peek += nonempty ? 1u : 0u;
+      const bool due = nonempty && (int32_t)((e >> 16) & 0x7fffu) <= ln.time;
+      if (__builtin_expect(due && cnt > cap, 0)) refill(x, ko, slot);
+      const uint32_t popped = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
+      PW(lay.w_chw + ko) = due ? popped : chw;
+      pick = due ? ((e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16)) : pick;
+      scanning = scanning && !due;
     }
-    const uint32_t popped = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
-    PW(lay.w_chw + ko) = due ? popped : chw;
-    pick = due ? ((e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16)) : pick;
-    scanning = scanning && !due;
+  } else if (act) {
+    bool done = false;
+#pragma unroll
+    for (int32_t ko = 0; ko < (unrolled(D) ? D : x.outdeg); ++ko) {
+      if (ko >= x.outdeg) break;
+      if (done) continue;
+      const uint32_t chw = PW(lay.w_chw + ko);
+      const uint32_t cnt = (chw >> 8) & 0xffu;
+      if (!cnt) {
+        empty_scanned |= 1u << ko;
+        continue;
+      }
+      ln.peek++;
+      const uint32_t head = chw & (cap - 1);
+      const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
+      const uint32_t e = PW(slot);
+      if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) continue;
+      if (__builtin_expect(cnt > cap, 0)) refill(x, ko, slot);
+      PW(lay.w_chw + ko) = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
+      pick = (e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16);
+      done = true;
+    }
   }
   XW(lay.x_pick + x.lane) = pick;
   wave_sync();
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
+  if constexpr (unrolled(D) && CLSNAP_B_PRED) {
 #pragma unroll
-  for (int32_t ki = 0; ki < D; ++ki) {
-    const uint32_t src = it[ki] & 0xffu;
-    const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
-    const bool m = act && ki < x.indeg && (pk & kPickValid) && ((pk >> 16) & 0x7fu) == ((it[ki] >> 8) & 0xffu);
-    const bool mk = m && (pk & kMarkerBit);
-    const bool tok = m && !mk;
-    const uint32_t pay = pk & 0xffffu;
-    // HandleToken: tokens += data; the channel's recording cursor advances
-    ln.tokens += tok ? (int32_t)pay : 0;
-    ln.pop_tok += tok ? 1u : 0u;
-    ln.pop_mk += mk ? 1u : 0u;
-    const uint32_t cur = PW(lay.w_cur + ki);
-    PW(lay.w_cur + ki) = cur + (tok ? 1u : 0u);
-    if (mk) handle_marker<D>(x, ln, it, ki, src, (int32_t)pay, ntrig);
+    for (int32_t ki = 0; ki < D; ++ki) {
+      if (ki >= lay.id) break;  // uniform: the layout holds id in-links per lane
+      const uint32_t w = it[ki];
+      const uint32_t src = w & 0xffu;
+      const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
+      const bool m = act && ki < x.indeg && (pk & kPickValid) && ((pk >> 16) & 0x7fu) == ((w >> 8) & 0xffu);
+      const bool mk = m && (pk & kMarkerBit);
+      const bool tok = m && !mk;
+      const uint32_t pay = pk & 0xffffu;
+      // HandleToken: tokens += data; the channel's recording cursor advances
+      ln.tokens += tok ? (int32_t)pay : 0;
+      ln.pop_tok += tok ? 1u : 0u;
+      ln.pop_mk += mk ? 1u : 0u;
+      const uint32_t cur = PW(lay.w_cur + ki);
+      PW(lay.w_cur + ki) = cur + (tok ? 1u : 0u);
+      if (mk) handle_marker<D>(x, ln, it, ki, src, (int32_t)pay, ntrig);
+    }
+  } else if (act) {
+#pragma unroll
+    for (int32_t ki = 0; ki < (unrolled(D) ? D : x.indeg); ++ki) {
+      if (ki >= x.indeg) break;
+      const uint32_t w = in_word<D>(x, it, ki);
+      const uint32_t src = w & 0xffu;
+      const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
+      if (!(pk & kPickValid) || ((pk >> 16) & 0x7fu) != ((w >> 8) & 0xffu)) continue;
+      const uint32_t pay = pk & 0xffffu;
+      if (!(pk & kMarkerBit)) {  // HandleToken: tokens += data; the recording cursor advances
+        ln.pop_tok++;
+        ln.tokens += (int32_t)pay;
+        PW(lay.w_cur + ki) += 1u;
+        continue;
+      }
+      ln.pop_mk++;
+      handle_marker<D>(x, ln, it, ki, src, (int32_t)pay, ntrig);
+    }
   }
   // ---- C/D: broadcast draws in sender order, then push -------------------------
   if (__ballot(ntrig > 0)) {
@@ -277,11 +366,17 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const uint32_t (&it
 // Occupancy target per degree bound (waves per SIMD; 256-thread workgroups).  Forcing
 // 8 waves/SIMD at D = 1 costs scratch spills; CLSNAP_OCC selects the policy (0 = let the
 // compiler choose, 1 = force the targets) -- an A/B knob, see DESIGN.md §9.
-#ifndef CLSNAP_OCC
-#define CLSNAP_OCC 0
+#ifndef CLSNAP_W1
+#define CLSNAP_W1 0  // waves/SIMD target for D = 1 (0 = compiler's choice)
+#endif
+#ifndef CLSNAP_W2
+#define CLSNAP_W2 0
+#endif
+#ifndef CLSNAP_W4
+#define CLSNAP_W4 0
 #endif
 constexpr int waves_for(int D) {
-  return CLSNAP_OCC ? (D <= 2 ? 8 : D <= 4 ? 6 : D <= 8 ? 4 : 2) : 1;
+  return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1) : D == 4 ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : 1;
 }
 
 template <int D>
@@ -303,7 +398,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   const uint32_t* nb = topo + (size_t)(valid ? v : 0) * p.topo_w;
   const int32_t indeg = valid ? (int32_t)nb[0] : 0;
   const int32_t outdeg = valid ? (int32_t)nb[1] : 0;
-  const uint64_t seg_mask = N == 64 ? ~0ull : (((1ull << N) - 1) << (seg * N));
   const uint32_t st = (uint32_t)p.stride;
   // Stage the wave's delay rows (ipw contiguous rows of sched_row bytes) in LDS when they fit.
   const bool staged = lay.x_delay > 0;
@@ -315,11 +409,15 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)first * p.sched_row);
     for (uint32_t k = lane; k < words; k += kWave) X[lay.x_delay + k] = src[k];
   }
-  const Ctx x{p, lay, X + lane, X, sched + (size_t)ii * p.sched_row, lrow, lane, seg * N, v, seg, ii, st, seg_mask,
+  const Ctx x{p, lay, X + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0};
-  uint32_t it[D];
+  InLinks<D> it;
+  if constexpr (unrolled(D)) {
 #pragma unroll
-  for (int32_t k = 0; k < D; ++k) it[k] = k < indeg ? nb[3 + k] : 0u;
+    for (int32_t k = 0; k < D; ++k) it[k] = k < indeg ? nb[3 + k] : 0u;
+  } else {
+    it[0] = 0;
+  }
 
   Lane ln;
   ln.flag = 0;
@@ -351,6 +449,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
       XW(lay.x_ndone + seg) = Dn[lay.s_cap * st];
     }
   }
+  if constexpr (!unrolled(D))
+    for (int32_t k = 0; k < indeg; ++k) PW(lay.w_int + k) = nb[3 + k];
   wave_sync();
   ln.alive = valid && ln.status == ST_OK;
   int32_t n_started = p.n_started_before;
@@ -554,17 +654,21 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
   return (int)hipGetLastError();
 }
 
-// The kernel is instantiated for degree bounds 1, 2, 4, 8, 16, 32, 64, 128.
+// The kernel is instantiated for degree bounds 1, 2, 4, ... CLSNAP_MAX_D.
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
-  const int32_t d = p.lay.od;  // the host sizes od == id == the power-of-two degree bound
+  const int32_t d = p.lay.od > p.lay.id ? p.lay.od : p.lay.id;  // D must bound every in- and out-degree
   if (d <= 1) return launch_exec_d<1>(p, topo, ops, sched, stream);
   if (d <= 2) return launch_exec_d<2>(p, topo, ops, sched, stream);
   if (d <= 4) return launch_exec_d<4>(p, topo, ops, sched, stream);
+#if CLSNAP_MAX_D >= 8
   if (d <= 8) return launch_exec_d<8>(p, topo, ops, sched, stream);
   if (d <= 16) return launch_exec_d<16>(p, topo, ops, sched, stream);
   if (d <= 32) return launch_exec_d<32>(p, topo, ops, sched, stream);
   if (d <= 64) return launch_exec_d<64>(p, topo, ops, sched, stream);
   return launch_exec_d<128>(p, topo, ops, sched, stream);
+#else
+  return (int)hipErrorNotSupported;
+#endif
 }
 
 int launch_checksums(const SumParams& p, void* stream) {

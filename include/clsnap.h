@@ -98,7 +98,8 @@ int cl_read_topology_text(cl_sim* sim, const char* text);
 /* Engine configuration (before the first flush). */
 int cl_set_device(cl_sim* sim, int32_t device_ordinal);
 /* fifo_lds_slots: per-channel packets kept in LDS (power of two, 2..64; deeper
- * channels spill to HBM).  max_drain_ticks bounds the drain loop (HANG status). */
+ * channels spill to HBM), or 0 to size it automatically for occupancy (default).
+ * max_drain_ticks bounds the drain loop (HANG status). */
 int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks);
 
 /* Delay source replacing rand.Intn(maxDelay) at sim.go:101.
