@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--instances", type=int, default=0, help="instances per GPU (default: config)")
     ap.add_argument("--fifo-slots", type=int, default=0, help="LDS ring slots per channel (0 = automatic)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -158,23 +158,27 @@ def main():
 
 
 def cpu_baseline(top, events, n_total, budget_s):
-    """The CPU oracle (C restatement, one simulation per thread) on a bounded sample of
-    the same workload: the first S instances with the same seeds."""
+    """The CPU oracle (C restatement, one simulation per thread) on the same instances
+    (same seeds), repeated in passes until about budget_s of CPU work has run."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = min(16, os.cpu_count() or 1)
     t_text = open(os.path.join(TEST_DATA, top)).read()
     e_text = open(os.path.join(TEST_DATA, events)).read()
-    probe = 2000
+    probe = min(n_total, 4096)
     secs, st, _, cnt, _ = O.run_batch(t_text, e_text, probe, threads=threads)
-    rate = probe / max(secs, 1e-6)
-    sample = int(min(n_total, max(probe, rate * budget_s)))
-    secs, st, _, cnt, _ = O.run_batch(t_text, e_text, sample, threads=threads)
-    ok = st == 0
-    pkts = int((cnt[ok, 2] + cnt[ok, 3]).sum())
-    return {"value": pkts / secs, "unit": "packets/s", "cores": threads, "kind": "port",
-            "sample": f"first {sample} of {n_total} instances (same seeds), {secs:.1f} s, "
-                      f"CPU restatement in C (oracle/cl_oracle.c), not the Go reference (no Go toolchain)"}
+    sample = int(min(n_total, max(probe, probe / max(secs, 1e-6) * budget_s)))
+    total_s, total_pkts, passes = 0.0, 0, 0
+    while passes == 0 or total_s < 0.5 * budget_s:
+        secs, st, _, cnt, _ = O.run_batch(t_text, e_text, sample, threads=threads)
+        ok = st == 0
+        total_pkts += int((cnt[ok, 2] + cnt[ok, 3]).sum())
+        total_s += secs
+        passes += 1
+    return {"value": total_pkts / total_s, "unit": "packets/s", "cores": threads, "kind": "port",
+            "sample": f"{passes} pass(es) over the first {sample} of {n_total} instances (same seeds), "
+                      f"{total_s:.1f} s; CPU restatement in C (oracle/cl_oracle.c), one simulation per "
+                      f"thread -- not the Go reference (no Go toolchain in the image)"}
 
 
 if __name__ == "__main__":

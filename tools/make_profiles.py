@@ -1,0 +1,63 @@
+"""Turn a gpurun_out/pmc_<cfg> directory into committed profile summaries.
+
+usage: python tools/make_profiles.py <round> <cfg> [instances]
+writes profiles/<round>_<cfg>_kernel_stats.csv  (rocprofv3 --kernel-trace --stats)
+       profiles/<round>_<cfg>_pmc.json          (per-dispatch PMC means, timed dispatches)
+       profiles/traffic_<cfg>.json              (HBM bytes per launch for bench.py)
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KB; FETCH_SIZE
+reads 1/2 of a wide coalesced stream on gfx950, so bytes = (2 * FETCH + WRITE) * 1024.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "cl_exec_kernel"
+
+
+def per_dispatch(paths):
+    vals = collections.defaultdict(dict)  # counter -> dispatch -> value
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            if KERNEL not in r["Kernel_Name"]:
+                continue
+            d = int(r["Dispatch_Id"])
+            vals[r["Counter_Name"]][d] = vals[r["Counter_Name"]].get(d, 0.0) + float(r["Counter_Value"])
+    return vals
+
+
+def main():
+    rnd, cfg = sys.argv[1], sys.argv[2]
+    inst = int(sys.argv[3]) if len(sys.argv) > 3 else {"c2": 65536, "c3": 131072}[cfg]
+    src = os.path.join(ROOT, "gpurun_out", f"pmc_{cfg}")
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    stats = os.path.join(src, "trace", "p_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(out, f"{rnd}_{cfg}_kernel_stats.csv"))
+    summary = {}
+    for name, per in per_dispatch(glob.glob(os.path.join(src, "pass*", "p_counter_collection.csv"))).items():
+        ds = sorted(per)
+        timed = ds[2:] if len(ds) > 2 else ds  # skip the first flush (writes state) and the warmup
+        summary[name] = sum(per[d] for d in timed) / len(timed)
+    with open(os.path.join(out, f"{rnd}_{cfg}_pmc.json"), "w") as f:
+        json.dump({"kernel": KERNEL, "config": cfg, "instances": inst,
+                   "note": "mean per timed dispatch; SQ_* cycle counters are quad-cycles",
+                   "counters": summary}, f, indent=1, sort_keys=True)
+    if "FETCH_SIZE" in summary and "WRITE_SIZE" in summary:
+        hbm = (2 * summary["FETCH_SIZE"] + summary["WRITE_SIZE"]) * 1024
+        with open(os.path.join(out, f"traffic_{cfg}.json"), "w") as f:
+            json.dump({"config": cfg, "instances": inst, "fifo_slots": 0,
+                       "hbm_bytes_per_launch": hbm, "fetch_kb": summary["FETCH_SIZE"],
+                       "write_kb": summary["WRITE_SIZE"], "round": rnd}, f, indent=1)
+    for row in csv.DictReader(open(stats)):
+        if KERNEL in row["Name"]:
+            print(cfg, "avg kernel ns", row["AverageNs"], "calls", row["Calls"])
+    print(json.dumps({k: round(v) for k, v in sorted(summary.items())}))
+
+
+if __name__ == "__main__":
+    main()
