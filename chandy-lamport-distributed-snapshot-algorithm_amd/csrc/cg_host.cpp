@@ -1,0 +1,1146 @@
+// cg_host.cpp -- host runtime of the graph engine behind include/clgraph.h.
+//
+// One cl_graph is ONE reference simulation (sim.go ChandyLamportSim) over a topology of
+// up to 2^31 nodes / channels whose state lives in HBM:
+//   * topology: AddNode/AddLink (or a bulk rank-ordered edge list, or the synthetic
+//     generators of SURVEY.md §8(d)) frozen into rank order (getSortedKeys,
+//     common.go:135-146): channels by (src rank, dest rank) = out-CSR, plus the in-CSR
+//     (dest rank, src rank) that recording cursors are laid out in;
+//   * events: SendTokens / StartSnapshot / Tick / drain (sim.go:58-123,
+//     test_common.go:79-140) append to a program; flush launches the per-tick kernel
+//     sequence of cg_kernels.hip for what is pending, rerun replays it from scratch;
+//   * delays: rand.Intn(5) at sim.go:101 is replaced by a pure function of the run's
+//     draw index (counter hash, Go math/rand stream, or an explicit schedule), so the
+//     reference's draw ORDER decides every delay;
+//   * results: snapshots are expanded back into the reference's {tokenMap, messages}
+//     shape (sim.go:134-173) from the recording cursors.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/clgraph.h"
+#include "cg_engine.h"
+#include "cl_text.h"
+
+using namespace clsnap;
+
+namespace {
+
+int gerr(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  const int rc = set_error_v(code, fmt, ap);
+  va_end(ap);
+  return rc;
+}
+
+#define GHIP(expr)                                                                      \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return gerr(CL_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+struct GBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int ensure(size_t count) {
+    if (count == 0) count = 1;
+    if (count <= n && p) return CL_OK;
+    release();
+    GHIP(hipMalloc((void**)&p, count * sizeof(T)));
+    n = count;
+    return CL_OK;
+  }
+  int upload(const std::vector<T>& v) {
+    int rc = ensure(v.size());
+    if (rc) return rc;
+    if (!v.empty()) GHIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return CL_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  size_t bytes() const { return n * sizeof(T); }
+};
+
+enum ProgKind : int32_t { P_SEND = 1, P_SNAP = 2, P_TICK = 3, P_DRAIN = 4 };
+struct ProgOp {
+  int32_t kind, a, b;
+  int64_t n;
+};
+
+inline uint64_t mulhi(uint64_t x, uint64_t n) { return (uint64_t)(((unsigned __int128)x * n) >> 64); }
+
+int digits(int64_t x) {
+  int d = 1;
+  while (x >= 10) {
+    x /= 10;
+    ++d;
+  }
+  return d;
+}
+
+constexpr int64_t kExtraDrainTicks = 6;  // maxDelay + 1 (test_common.go:135-137)
+constexpr int64_t kMaxGraphTime = (1 << 25) - 8;  // pick words hold (tick << 6) | out-index
+
+}  // namespace
+
+struct cl_graph {
+  int device = 0;
+
+  // ---- topology ------------------------------------------------------------
+  std::vector<std::string> ids;  // insertion order (string mode)
+  std::vector<int64_t> init_tokens;
+  std::unordered_map<std::string, int> id_index;
+  std::vector<std::pair<int, int>> links;
+  bool bulk = false;  // ids are "N" + zero-padded rank
+  int id_width = 0;
+  bool frozen = false;
+  int32_t n = 0;
+  int64_t e = 0;
+  std::vector<int32_t> rank_of, by_rank;
+  std::vector<int32_t> out_off, ch_dst, ch_src, ch_inpos, in_off, in_src, init_tok;
+  int64_t total_tokens = 0;
+  int32_t max_out = 0, max_in = 0;
+
+  // ---- configuration -------------------------------------------------------
+  int32_t cap_log2 = 4;
+  int32_t max_snaps_cfg = 0;
+  int64_t max_drain = 10000;
+  int32_t delay_mode = 0;  // 0 hash, 1 schedule (Go seed or explicit)
+  uint64_t delay_seed = 0;
+  bool go_seed = false;
+  int64_t go_seed_val = 0;
+  std::vector<uint8_t> user_sched;
+  uint64_t traffic_seed = 0;
+  uint32_t traffic_thresh = 0;
+  int64_t traffic_steps = 0;
+
+  // ---- program ---------------------------------------------------------------
+  std::vector<ProgOp> prog;
+  std::vector<GOp> gops;  // SEND/SNAP ops in program order
+  int32_t n_sids = 0;
+  int64_t host_sends = 0;
+  std::vector<int32_t> ch_sends;  // host sends per channel
+  bool nonunit = false;           // a host send moves != 1 token: keep payload history
+
+  // ---- execution -------------------------------------------------------------
+  size_t executed = 0;     // program ops executed on the device state
+  size_t gop_cursor = 0;   // gops executed
+  int64_t time = 0;        // host view of the simulator time
+  bool hang = false;
+  bool state_valid = false;
+  bool dev_ready = false;
+  hipStream_t stream = nullptr;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  size_t ev_used = 0;
+  double run_ms = 0;
+  int64_t runs = 0, run_ticks = 0, pending_ticks = 0;
+
+  GParams P{};
+  int32_t s_cap = 0, hist = 0, lanes = 1, alloc_cap_log2 = -1;
+  int64_t sched_len = 0;
+  GBuf<int32_t> d_out_off, d_ch_dst, d_ch_inpos, d_in_off, d_in_src, d_init_tok;
+  GBuf<int32_t> d_tokens, d_pick, d_trig, d_ltrig, d_lsend, d_crn, d_mlist, d_xl;
+  GBuf<uint64_t> d_mask, d_cre;
+  GBuf<long long> d_bsum;
+  GBuf<uint32_t> d_hc, d_tokcnt, d_histv;
+  GBuf<uint64_t> d_fifo, d_deliv, d_W, d_rec;
+  GBuf<int32_t> d_cnt, d_stok, d_done, d_ctick;
+  GBuf<GScal> d_sc;
+  GBuf<GOp> d_ops;
+  GBuf<uint8_t> d_sched;
+  GBuf<unsigned long long> d_scratch;
+  size_t ops_uploaded = 0;
+
+  ~cl_graph() {
+    if (!dev_ready) return;
+    (void)hipSetDevice(device);
+    (void)hipStreamSynchronize(stream);
+    GBuf<int32_t>* i32s[] = {&d_out_off, &d_ch_dst, &d_ch_inpos, &d_in_off, &d_in_src, &d_init_tok, &d_tokens,
+                             &d_pick,    &d_trig,   &d_ltrig,    &d_lsend,  &d_crn,    &d_mlist,    &d_xl,
+                             &d_cnt,     &d_stok,   &d_done,     &d_ctick};
+    for (auto* b : i32s) b->release();
+    d_mask.release(); d_cre.release(); d_bsum.release(); d_hc.release(); d_tokcnt.release(); d_histv.release();
+    d_fifo.release(); d_deliv.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
+    d_sched.release(); d_scratch.release();
+    for (auto& ev : ev_pool) {
+      (void)hipEventDestroy(ev.first);
+      (void)hipEventDestroy(ev.second);
+    }
+    (void)hipStreamDestroy(stream);
+  }
+
+  // ---- topology --------------------------------------------------------------
+  std::string node_id(int32_t r) const {
+    if (bulk) {
+      char buf[32];
+      snprintf(buf, sizeof buf, "N%0*d", id_width, r);
+      return buf;
+    }
+    return ids[by_rank[r]];
+  }
+
+  // rank of an id, -1 if unknown
+  int32_t rank_of_id(const char* id) const {
+    if (!id) return -1;
+    if (bulk) {
+      const size_t L = std::strlen(id);
+      if (L != (size_t)id_width + 1 || id[0] != 'N') return -1;
+      int64_t v = 0;
+      for (size_t i = 1; i < L; ++i) {
+        if (id[i] < '0' || id[i] > '9') return -1;
+        v = v * 10 + (id[i] - '0');
+      }
+      return v < n ? (int32_t)v : -1;
+    }
+    auto it = id_index.find(id);
+    if (it == id_index.end()) return -1;
+    return frozen ? rank_of[it->second] : it->second;
+  }
+
+  // channels (src rank, dst rank), sorted and unique -> CSR
+  int build_csr(std::vector<std::pair<int32_t, int32_t>>& ch) {
+    std::sort(ch.begin(), ch.end());
+    ch.erase(std::unique(ch.begin(), ch.end()), ch.end());
+    if (ch.size() >= (size_t)INT32_MAX) return gerr(CL_E_LIMIT, "too many channels");
+    e = (int64_t)ch.size();
+    out_off.assign(n + 1, 0);
+    in_off.assign(n + 1, 0);
+    ch_src.resize(e);
+    ch_dst.resize(e);
+    for (int64_t c = 0; c < e; ++c) {
+      ch_src[c] = ch[c].first;
+      ch_dst[c] = ch[c].second;
+      out_off[ch[c].first + 1]++;
+      in_off[ch[c].second + 1]++;
+    }
+    for (int32_t v = 0; v < n; ++v) {
+      out_off[v + 1] += out_off[v];
+      in_off[v + 1] += in_off[v];
+    }
+    ch_inpos.resize(e);
+    in_src.resize(e);
+    std::vector<int32_t> fill(in_off.begin(), in_off.end() - 1);
+    for (int64_t c = 0; c < e; ++c) {  // channels sorted by src: in-lists come out by src rank
+      const int32_t k = fill[ch_dst[c]]++;
+      ch_inpos[c] = k;
+      in_src[k] = ch_src[c];
+    }
+    max_out = max_in = 0;
+    for (int32_t v = 0; v < n; ++v) {
+      max_out = std::max(max_out, out_off[v + 1] - out_off[v]);
+      max_in = std::max(max_in, in_off[v + 1] - in_off[v]);
+    }
+    if (max_out > kGMaxOutDegree)
+      return gerr(CL_E_LIMIT, "out-degree %d exceeds the graph engine's %d", max_out, kGMaxOutDegree);
+    ch_sends.assign(e, 0);
+    frozen = true;
+    return CL_OK;
+  }
+
+  int freeze() {
+    if (frozen) return CL_OK;
+    n = (int32_t)ids.size();
+    by_rank.resize(n);
+    std::iota(by_rank.begin(), by_rank.end(), 0);
+    std::sort(by_rank.begin(), by_rank.end(), [&](int a, int b) { return ids[a] < ids[b]; });
+    rank_of.assign(n, 0);
+    for (int r = 0; r < n; ++r) rank_of[by_rank[r]] = r;
+    init_tok.resize(n);
+    total_tokens = 0;
+    for (int r = 0; r < n; ++r) {
+      init_tok[r] = (int32_t)init_tokens[by_rank[r]];
+      total_tokens += init_tokens[by_rank[r]];
+    }
+    std::vector<std::pair<int32_t, int32_t>> ch;
+    ch.reserve(links.size());
+    for (auto& l : links) ch.emplace_back(rank_of[l.first], rank_of[l.second]);
+    return build_csr(ch);
+  }
+
+  int set_topology(int32_t nn, int32_t width, const int64_t* tokens, int64_t m, const int32_t* src,
+                   const int32_t* dst) {
+    if (frozen || !ids.empty()) return gerr(CL_E_STATE, "the topology is already set");
+    if (nn <= 0 || !tokens || (m > 0 && (!src || !dst)) || m < 0) return gerr(CL_E_INVALID, "bad topology arrays");
+    if (width == 0) width = digits(nn - 1);
+    if (width < digits(nn - 1) || width > 10)
+      return gerr(CL_E_INVALID, "id width %d cannot keep %d ranks in lexicographic order", width, nn);
+    n = nn;
+    bulk = true;
+    id_width = width;
+    init_tok.resize(n);
+    total_tokens = 0;
+    for (int32_t r = 0; r < n; ++r) {
+      if (tokens[r] < 0 || tokens[r] > INT32_MAX) return gerr(CL_E_LIMIT, "token count out of range");
+      init_tok[r] = (int32_t)tokens[r];
+      total_tokens += tokens[r];
+    }
+    if (total_tokens > INT32_MAX) return gerr(CL_E_LIMIT, "total tokens exceed int32");
+    std::vector<std::pair<int32_t, int32_t>> ch;
+    ch.reserve((size_t)m);
+    for (int64_t i = 0; i < m; ++i) {
+      if (src[i] < 0 || src[i] >= n || dst[i] < 0 || dst[i] >= n)
+        return gerr(CL_E_UNKNOWN_NODE, "edge %lld references a rank outside [0, %d)", (long long)i, n);
+      if (src[i] != dst[i]) ch.emplace_back(src[i], dst[i]);  // node.go:88-90
+    }
+    return build_csr(ch);
+  }
+
+  // ---- program -------------------------------------------------------------------
+  int append_send(int32_t a, int32_t b, int64_t nt) {
+    if (nt < 0 || nt > (int64_t)kGPayload) return gerr(CL_E_LIMIT, "token count %lld out of range", (long long)nt);
+    if (nt != 1) nonunit = true;
+    if (b >= 0) {
+      // out-index lookup only to count per-channel sends (history sizing)
+      auto lo = ch_dst.begin() + out_off[a], hi = ch_dst.begin() + out_off[a + 1];
+      auto it = std::lower_bound(lo, hi, b);
+      if (it != hi && *it == b) ch_sends[it - ch_dst.begin()]++;
+    }
+    host_sends++;
+    prog.push_back(ProgOp{P_SEND, a, b, nt});
+    gops.push_back(GOp{GOP_SEND, a, b, (int32_t)nt});
+    return CL_OK;
+  }
+
+  int append_snap(int32_t a, int32_t* out_sid) {
+    if (n_sids == INT32_MAX) return gerr(CL_E_LIMIT, "too many snapshots");
+    const int32_t sid = n_sids++;
+    if (out_sid) *out_sid = sid;
+    prog.push_back(ProgOp{P_SNAP, a, sid, 0});
+    gops.push_back(GOp{GOP_SNAP, a, sid, 0});
+    return CL_OK;
+  }
+
+  int append_tick(int64_t k) {
+    if (k <= 0) return CL_OK;
+    pending_ticks += k;
+    if (!prog.empty() && prog.back().kind == P_TICK && executed < prog.size()) {
+      prog.back().n += k;
+      return CL_OK;
+    }
+    prog.push_back(ProgOp{P_TICK, 0, 0, k});
+    return CL_OK;
+  }
+
+  // ---- device ----------------------------------------------------------------------
+  int ensure_device() {
+    if (dev_ready) return CL_OK;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+      return gerr(CL_E_DEVICE, "no HIP device available (the engine needs a gfx950 GPU)");
+    if (device < 0 || device >= count) return gerr(CL_E_DEVICE, "device %d out of range (%d)", device, count);
+    GHIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    GHIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      return gerr(CL_E_DEVICE, "device %d is %s, the engine is built for gfx950", device, prop.gcnArchName);
+    GHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    dev_ready = true;
+    int rc;
+    if ((rc = d_out_off.upload(out_off)) || (rc = d_ch_dst.upload(ch_dst)) || (rc = d_ch_inpos.upload(ch_inpos)) ||
+        (rc = d_in_off.upload(in_off)) || (rc = d_in_src.upload(in_src)) || (rc = d_init_tok.upload(init_tok)))
+      return rc;
+    return CL_OK;
+  }
+
+  int32_t hist_needed() const {
+    if (!nonunit) return 0;
+    int64_t mx = 0;
+    for (auto c : ch_sends) mx = std::max<int64_t>(mx, c);
+    mx += traffic_steps;
+    int32_t h = 16;
+    while (h < mx) h <<= 1;
+    return h;
+  }
+
+  int64_t draws_bound() const {
+    return host_sends + traffic_steps * (int64_t)n + (int64_t)n_sids * e;
+  }
+
+  // (Re)allocate the run state when the program outgrew it. Returns 1 in *realloc when
+  // the device state was reallocated (the program must then be replayed from the start).
+  int ensure_state(bool* reallocated) {
+    *reallocated = false;
+    const int32_t want_s = std::max({n_sids, max_snaps_cfg, 16});
+    const int32_t want_h = hist_needed();
+    if (s_cap >= n_sids && hist >= want_h && alloc_cap_log2 == cap_log2 && d_sc.p) return CL_OK;
+    *reallocated = true;
+    s_cap = std::max(s_cap, want_s);
+    hist = std::max(hist, want_h);
+    alloc_cap_log2 = cap_log2;
+    const size_t N = (size_t)n, E = (size_t)std::max<int64_t>(e, 1);
+    if ((uint64_t)s_cap * N >= (1ull << 40) || (uint64_t)s_cap * E >= (1ull << 40))
+      return gerr(CL_E_LIMIT, "snapshot state too large");
+    int rc;
+    if ((rc = d_tokens.ensure(N)) || (rc = d_pick.ensure(N)) || (rc = d_trig.ensure(N)) || (rc = d_ltrig.ensure(N)) ||
+        (rc = d_lsend.ensure(N)) || (rc = d_crn.ensure(N)) || (rc = d_mlist.ensure(N)) || (rc = d_xl.ensure(N)) ||
+        (rc = d_mask.ensure(N)) || (rc = d_cre.ensure(E)) || (rc = d_bsum.ensure(2 * ((N + kTallyBlock - 1) / kTallyBlock))) ||
+        (rc = d_hc.ensure(E)) || (rc = d_tokcnt.ensure(E)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
+        (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_deliv.ensure(E)) || (rc = d_W.ensure(s_cap * N)) ||
+        (rc = d_rec.ensure(s_cap * E)) || (rc = d_cnt.ensure(s_cap * N)) || (rc = d_stok.ensure(s_cap * N)) ||
+        (rc = d_done.ensure(s_cap)) || (rc = d_ctick.ensure(s_cap)) || (rc = d_sc.ensure(1)) ||
+        (rc = d_scratch.ensure(3 + (size_t)s_cap)))
+      return rc;
+    return CL_OK;
+  }
+
+  int ensure_sched() {
+    if (delay_mode == 0) {
+      sched_len = 0;
+      return CL_OK;
+    }
+    if (!go_seed) {
+      if ((int64_t)d_sched.n >= (int64_t)user_sched.size() && sched_len == (int64_t)user_sched.size()) return CL_OK;
+      sched_len = (int64_t)user_sched.size();
+      return d_sched.upload(user_sched);
+    }
+    const int64_t need = std::max<int64_t>(16, draws_bound());
+    if (sched_len >= need) return CL_OK;
+    std::vector<uint8_t> s((size_t)need);
+    int rc = cl_go_delay_schedule(go_seed_val, 1, need, s.data());  // instance 0 of the Go streams
+    if (rc) return rc;
+    if ((rc = d_sched.upload(s))) return rc;
+    sched_len = need;
+    return CL_OK;
+  }
+
+  void fill_params() {
+    GParams& p = P;
+    p.n = n;
+    p.e = (int32_t)e;
+    p.cap_log2 = cap_log2;
+    p.s_cap = s_cap;
+    p.hist = hist;
+    p.delay_mode = delay_mode;
+    p.delay_seed = delay_seed;
+    p.sched = d_sched.p;
+    p.sched_len = sched_len;
+    p.traffic_seed = traffic_seed;
+    p.traffic_thresh = traffic_thresh;
+    p.traffic_steps = traffic_steps;
+    p.n_blocks = (n + kTallyBlock - 1) / kTallyBlock;
+    p.out_off = d_out_off.p;
+    p.ch_dst = d_ch_dst.p;
+    p.ch_inpos = d_ch_inpos.p;
+    p.in_off = d_in_off.p;
+    p.in_src = d_in_src.p;
+    p.tokens = d_tokens.p;
+    p.mask = d_mask.p;
+    p.pick = d_pick.p;
+    p.trig = d_trig.p;
+    p.ltrig = d_ltrig.p;
+    p.lsend = d_lsend.p;
+    p.bsum = d_bsum.p;
+    p.crn = d_crn.p;
+    p.cre = d_cre.p;
+    p.mlist = d_mlist.p;
+    p.xl = d_xl.p;
+    p.hc = d_hc.p;
+    p.fifo = d_fifo.p;
+    p.tokcnt = d_tokcnt.p;
+    p.deliv = d_deliv.p;
+    p.histv = d_histv.p;
+    p.W = d_W.p;
+    p.cnt = d_cnt.p;
+    p.stok = d_stok.p;
+    p.rec = d_rec.p;
+    p.done = d_done.p;
+    p.ctick = d_ctick.p;
+    p.sc = d_sc.p;
+    p.ops = d_ops.p;
+    // lanes per created local snapshot in k_expand: about the mean in-degree
+    const int64_t mean = e > 0 ? (e + n - 1) / n : 1;
+    lanes = 1;
+    while (lanes < mean && lanes < 64) lanes <<= 1;
+  }
+
+  int upload_ops() {
+    if (gops.size() == ops_uploaded && d_ops.p) return CL_OK;
+    int rc = d_ops.ensure(std::max<size_t>(gops.size(), 64));
+    if (rc) return rc;
+    if (!gops.empty()) GHIP(hipMemcpy(d_ops.p, gops.data(), gops.size() * sizeof(GOp), hipMemcpyHostToDevice));
+    ops_uploaded = gops.size();
+    return CL_OK;
+  }
+
+  int k_err(int e_) {
+    if (e_) return gerr(CL_E_DEVICE, "graph kernel launch failed: %s", hipGetErrorString((hipError_t)e_));
+    return CL_OK;
+  }
+
+  int launch_tick() {
+    if (time + 1 > kMaxGraphTime) return gerr(CL_E_LIMIT, "simulated time would exceed %lld ticks", (long long)kMaxGraphTime);
+    ++time;
+    ++run_ticks;
+    return k_err(cg_launch_tick(P, (int32_t)time, lanes, stream));
+  }
+
+  int flush_hostops(size_t& pend_begin, size_t& pend_count) {
+    if (!pend_count) return CL_OK;
+    int rc = k_err(cg_launch_hostops(P, (int32_t)time, (int32_t)pend_begin, (int32_t)pend_count, stream));
+    pend_begin += pend_count;
+    pend_count = 0;
+    return rc;
+  }
+
+  int read_status(int32_t* st) {
+    GScal sc;
+    GHIP(hipMemcpyAsync(&sc, d_sc.p, sizeof sc, hipMemcpyDeviceToHost, stream));
+    GHIP(hipStreamSynchronize(stream));
+    *st = sc.status;
+    return CL_OK;
+  }
+
+  // test_common.go:123-137: tick until all started snapshots completed, then +6.
+  int run_drain() {
+    std::vector<int32_t> ct((size_t)std::max(n_sids, 1));
+    int64_t ticks = 0;
+    for (;;) {
+      int32_t st;
+      int rc = read_status(&st);
+      if (rc) return rc;
+      if (st) return CL_OK;
+      bool all = true;
+      if (n_sids) {
+        GHIP(hipMemcpy(ct.data(), d_ctick.p, (size_t)n_sids * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int32_t s = 0; s < n_sids; ++s) all = all && ct[s] >= 0;
+      }
+      if (all) break;
+      if (ticks >= max_drain) {
+        hang = true;
+        return CL_OK;
+      }
+      if ((rc = launch_tick())) return rc;
+      ++ticks;
+    }
+    for (int64_t i = 0; i < kExtraDrainTicks; ++i) {
+      int rc = launch_tick();
+      if (rc) return rc;
+    }
+    return CL_OK;
+  }
+
+  // Execute program ops [executed, end) on the device; from scratch if `fresh`.
+  int run(bool fresh) {
+    int rc = freeze();
+    if (rc) return rc;
+    if (n == 0) return gerr(CL_E_STATE, "the topology has no nodes");
+    if ((rc = ensure_device())) return rc;
+    GHIP(hipSetDevice(device));
+    // buffers are only replaced between runs: wait for the previous one first
+    if (gops.size() != ops_uploaded || !state_valid) GHIP(hipStreamSynchronize(stream));
+    bool realloc = false;
+    if ((rc = ensure_state(&realloc))) return rc;
+    if ((rc = ensure_sched()) || (rc = upload_ops())) return rc;
+    fill_params();
+    if (realloc || !state_valid) fresh = true;
+    if (!fresh && executed == prog.size()) return CL_OK;
+    if (ev_used == ev_pool.size()) {
+      std::pair<hipEvent_t, hipEvent_t> pr;
+      GHIP(hipEventCreate(&pr.first));
+      GHIP(hipEventCreate(&pr.second));
+      ev_pool.push_back(pr);
+    }
+    auto& ev = ev_pool[ev_used++];
+    GHIP(hipEventRecord(ev.first, stream));
+    size_t begin = executed;
+    if (fresh) {
+      begin = 0;
+      gop_cursor = 0;
+      time = 0;
+      hang = false;
+      if ((rc = k_err(cg_launch_reset(P, d_init_tok.p, stream)))) return rc;
+      if (traffic_steps > 0 && (rc = k_err(cg_launch_sends(P, 0, stream)))) return rc;  // step 0 traffic
+    }
+    state_valid = false;
+    size_t pend_begin = gop_cursor, pend_count = 0;
+    for (size_t i = begin; i < prog.size(); ++i) {
+      const ProgOp& op = prog[i];
+      if (op.kind == P_SEND || op.kind == P_SNAP) {
+        ++pend_count;
+      } else if (op.kind == P_TICK) {
+        if ((rc = flush_hostops(pend_begin, pend_count))) return rc;
+        for (int64_t k = 0; k < op.n; ++k)
+          if ((rc = launch_tick())) return rc;
+      } else if (op.kind == P_DRAIN) {
+        if ((rc = flush_hostops(pend_begin, pend_count))) return rc;
+        if ((rc = run_drain())) return rc;
+      }
+    }
+    if ((rc = flush_hostops(pend_begin, pend_count))) return rc;
+    GHIP(hipEventRecord(ev.second, stream));
+    gop_cursor = pend_begin;
+    executed = prog.size();
+    state_valid = true;
+    ++runs;
+    return CL_OK;
+  }
+
+  int sync() {
+    if (!dev_ready) return CL_OK;
+    GHIP(hipSetDevice(device));
+    GHIP(hipStreamSynchronize(stream));
+    return CL_OK;
+  }
+
+  int flush() {
+    int rc = CL_OK;
+    if (!frozen || !state_valid || executed != prog.size()) rc = run(false);
+    if (rc) return rc;
+    return sync();
+  }
+
+  int fold_time(double* total_ms, int64_t* nruns, int64_t* nticks) {
+    int rc = sync();
+    if (rc) return rc;
+    double ms = 0;
+    for (size_t i = 0; i < ev_used; ++i) {
+      float f = 0.f;
+      GHIP(hipEventElapsedTime(&f, ev_pool[i].first, ev_pool[i].second));
+      ms += f;
+    }
+    ev_used = 0;
+    *total_ms = ms;
+    *nruns = runs;
+    *nticks = run_ticks;
+    runs = 0;
+    run_ticks = 0;
+    return CL_OK;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+#define G_CHECK(g)                                                     \
+  do {                                                                 \
+    if (!(g)) return gerr(CL_E_INVALID, "null cl_graph handle");       \
+  } while (0)
+#define G_TOPO_OPEN(g)                                                                       \
+  do {                                                                                       \
+    if ((g)->frozen) return gerr(CL_E_STATE, "topology changes after events are not supported"); \
+  } while (0)
+
+extern "C" {
+
+uint64_t cl_counter_hash(uint64_t seed, uint64_t a, uint64_t b) { return cg_hash(seed, a, b); }
+
+int cl_graph_create(cl_graph** out) {
+  if (!out) return gerr(CL_E_INVALID, "null output");
+  *out = new cl_graph();
+  return CL_OK;
+}
+
+int cl_graph_destroy(cl_graph* g) {
+  delete g;
+  return CL_OK;
+}
+
+int cl_graph_set_device(cl_graph* g, int32_t device_ordinal) {
+  G_CHECK(g);
+  if (g->dev_ready) return gerr(CL_E_STATE, "device already selected");
+  g->device = device_ordinal;
+  return CL_OK;
+}
+
+int cl_graph_add_node(cl_graph* g, const char* id, int64_t tokens) {
+  G_CHECK(g);
+  G_TOPO_OPEN(g);
+  if (g->bulk) return gerr(CL_E_STATE, "bulk topology already set");
+  if (!id) return gerr(CL_E_INVALID, "null id");
+  if (g->id_index.count(id)) return gerr(CL_E_DUPLICATE_NODE, "node %s already exists", id);
+  if (tokens < 0 || tokens > INT32_MAX) return gerr(CL_E_LIMIT, "token count out of range");
+  g->total_tokens += tokens;
+  if (g->total_tokens > INT32_MAX) return gerr(CL_E_LIMIT, "total tokens exceed int32");
+  g->id_index[id] = (int)g->ids.size();
+  g->ids.emplace_back(id);
+  g->init_tokens.push_back(tokens);
+  return CL_OK;
+}
+
+int cl_graph_add_link(cl_graph* g, const char* src, const char* dest) {
+  G_CHECK(g);
+  const int a = g->rank_of_id(src), b = g->rank_of_id(dest);
+  if (a < 0) return gerr(CL_E_UNKNOWN_NODE, "Node %s does not exist", src ? src : "(null)");  // sim.go:49-51
+  if (b < 0) return gerr(CL_E_UNKNOWN_NODE, "Node %s does not exist", dest ? dest : "(null)");  // sim.go:52-54
+  G_TOPO_OPEN(g);
+  if (a != b) g->links.emplace_back(a, b);  // node.go:88-90; duplicates collapse at freeze
+  return CL_OK;
+}
+
+int cl_graph_read_topology_text(cl_graph* g, const char* text) {
+  G_CHECK(g);
+  if (!text) return gerr(CL_E_INVALID, "null text");
+  int64_t left = -1;
+  for (const std::string& line : go_lines(text)) {
+    if (!line.empty() && line[0] == '#') continue;
+    if (left < 0) {
+      if (!go_atoi(line, &left)) return gerr(CL_E_PARSE, "bad node count line: %s", line.c_str());
+      continue;
+    }
+    auto f = go_fields(line);
+    if (f.size() != 2) return gerr(CL_E_PARSE, "Expected 2 tokens in line: %s", line.c_str());
+    int rc;
+    if (left > 0) {
+      int64_t tok;
+      if (!go_atoi(f[1], &tok)) return gerr(CL_E_PARSE, "bad token count: %s", f[1].c_str());
+      if ((rc = cl_graph_add_node(g, f[0].c_str(), tok))) return rc;
+      left--;
+    } else if ((rc = cl_graph_add_link(g, f[0].c_str(), f[1].c_str()))) {
+      return rc;
+    }
+  }
+  return CL_OK;
+}
+
+int cl_graph_read_topology_file(cl_graph* g, const char* path) {
+  G_CHECK(g);
+  std::string text;
+  if (!path || !read_file(path, &text)) return gerr(CL_E_IO, "cannot read %s", path ? path : "(null)");
+  return cl_graph_read_topology_text(g, text.c_str());
+}
+
+int cl_graph_set_topology(cl_graph* g, int32_t n_nodes, int32_t id_width, const int64_t* tokens, int64_t n_edges,
+                          const int32_t* src, const int32_t* dst) {
+  G_CHECK(g);
+  return g->set_topology(n_nodes, id_width, tokens, n_edges, src, dst);
+}
+
+int cl_graph_generate_regular(cl_graph* g, int32_t n_nodes, int32_t degree, int64_t tokens, uint64_t seed) {
+  G_CHECK(g);
+  if (n_nodes <= 0 || degree < 0 || degree > kGMaxOutDegree) return gerr(CL_E_INVALID, "bad regular graph size");
+  const size_t N = (size_t)n_nodes;
+  std::vector<int32_t> src(N * degree), dst(N * degree);
+  std::vector<std::thread> th;
+  for (int p = 0; p < degree; ++p) {
+    th.emplace_back([&, p] {
+      std::vector<int32_t> perm(N);
+      std::iota(perm.begin(), perm.end(), 0);
+      for (size_t i = N - 1; i >= 1; --i) {  // Fisher-Yates
+        const size_t j = (size_t)mulhi(cg_hash(seed, (uint64_t)p, (uint64_t)i), (uint64_t)(i + 1));
+        std::swap(perm[i], perm[j]);
+      }
+      for (size_t v = 0; v < N; ++v) {
+        src[(size_t)p * N + v] = (int32_t)v;
+        dst[(size_t)p * N + v] = perm[v];
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  std::vector<int64_t> tok(N, tokens);
+  return g->set_topology(n_nodes, 0, tok.data(), (int64_t)src.size(), src.data(), dst.data());
+}
+
+int cl_graph_generate_powerlaw(cl_graph* g, int32_t n_nodes, int32_t targets, double exponent, int32_t ring,
+                               int64_t tokens, uint64_t seed) {
+  G_CHECK(g);
+  if (n_nodes <= 0 || targets < 0 || targets > kGMaxOutDegree - 2) return gerr(CL_E_INVALID, "bad power-law graph size");
+  const size_t N = (size_t)n_nodes;
+  std::vector<double> cdf(N);
+  double acc = 0;
+  for (size_t k = 0; k < N; ++k) {
+    acc += std::pow((double)(k + 1), -exponent);
+    cdf[k] = acc;
+  }
+  const double total = acc;
+  std::vector<int32_t> src, dst;
+  src.reserve(N * (targets + 2));
+  dst.reserve(N * (targets + 2));
+  for (size_t v = 0; v < N; ++v) {
+    for (int i = 0; i < targets; ++i) {
+      const uint64_t u = cg_hash(seed, (uint64_t)v, (uint64_t)i);
+      const double r = (double)(u >> 11) * (1.0 / 9007199254740992.0) * total;
+      size_t k = (size_t)(std::upper_bound(cdf.begin(), cdf.end(), r) - cdf.begin());
+      if (k >= N) k = N - 1;
+      src.push_back((int32_t)v);
+      dst.push_back((int32_t)k);
+    }
+  }
+  if (ring) {
+    for (size_t v = 0; v < N; ++v) {
+      src.push_back((int32_t)v);
+      dst.push_back((int32_t)((v + 1) % N));
+      src.push_back((int32_t)v);
+      dst.push_back((int32_t)((v + N - 1) % N));
+    }
+  }
+  std::vector<int64_t> tok(N, tokens);
+  return g->set_topology(n_nodes, 0, tok.data(), (int64_t)src.size(), src.data(), dst.data());
+}
+
+int cl_graph_num_nodes(cl_graph* g, int32_t* n) {
+  G_CHECK(g);
+  if (!n) return gerr(CL_E_INVALID, "null output");
+  int rc = g->freeze();
+  if (rc) return rc;
+  *n = g->n;
+  return CL_OK;
+}
+
+int cl_graph_num_channels(cl_graph* g, int64_t* n) {
+  G_CHECK(g);
+  if (!n) return gerr(CL_E_INVALID, "null output");
+  int rc = g->freeze();
+  if (rc) return rc;
+  *n = g->e;
+  return CL_OK;
+}
+
+int cl_graph_channels(cl_graph* g, int32_t* src, int32_t* dst) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  if (src) std::copy(g->ch_src.begin(), g->ch_src.end(), src);
+  if (dst) std::copy(g->ch_dst.begin(), g->ch_dst.end(), dst);
+  return CL_OK;
+}
+
+int cl_graph_node_id(cl_graph* g, int32_t rank, char* buf, int32_t cap) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  if (rank < 0 || rank >= g->n || !buf || cap <= 0) return gerr(CL_E_INVALID, "bad rank or buffer");
+  const std::string s = g->node_id(rank);
+  if ((int32_t)s.size() >= cap) return gerr(CL_E_LIMIT, "buffer too small");
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return CL_OK;
+}
+
+int cl_graph_set_limits(cl_graph* g, int32_t fifo_slots, int32_t max_snapshots, int64_t max_drain_ticks) {
+  G_CHECK(g);
+  int l = 0;
+  while ((1 << l) < fifo_slots) ++l;
+  if (fifo_slots < 2 || fifo_slots > 32768 || (1 << l) != fifo_slots)
+    return gerr(CL_E_INVALID, "fifo_slots must be a power of two in [2, 32768]");
+  if (max_snapshots < 0 || max_drain_ticks < 0) return gerr(CL_E_INVALID, "negative limit");
+  if (l != g->cap_log2) g->state_valid = false;
+  g->cap_log2 = l;
+  g->max_snaps_cfg = max_snapshots;
+  g->max_drain = max_drain_ticks;
+  return CL_OK;
+}
+
+int cl_graph_set_delay_hash(cl_graph* g, uint64_t seed) {
+  G_CHECK(g);
+  g->delay_mode = 0;
+  g->delay_seed = seed;
+  g->go_seed = false;
+  g->state_valid = false;
+  return CL_OK;
+}
+
+int cl_graph_set_delay_go_seed(cl_graph* g, int64_t seed) {
+  G_CHECK(g);
+  g->delay_mode = 1;
+  g->go_seed = true;
+  g->go_seed_val = seed;
+  g->sched_len = 0;
+  g->state_valid = false;
+  return CL_OK;
+}
+
+int cl_graph_set_delay_schedule(cl_graph* g, const uint8_t* delays, int64_t n) {
+  G_CHECK(g);
+  if (!delays || n <= 0) return gerr(CL_E_INVALID, "empty schedule");
+  for (int64_t i = 0; i < n; ++i)
+    if (delays[i] >= 5) return gerr(CL_E_INVALID, "delay %u at %lld outside [0, maxDelay)", delays[i], (long long)i);
+  g->user_sched.assign(delays, delays + n);
+  g->delay_mode = 1;
+  g->go_seed = false;
+  g->sched_len = -1;
+  g->state_valid = false;
+  return CL_OK;
+}
+
+int cl_graph_set_traffic(cl_graph* g, uint64_t seed, uint32_t threshold, int64_t steps) {
+  G_CHECK(g);
+  if (steps < 0) return gerr(CL_E_INVALID, "negative traffic steps");
+  g->traffic_seed = seed;
+  g->traffic_thresh = threshold;
+  g->traffic_steps = threshold ? steps : 0;
+  g->state_valid = false;
+  return CL_OK;
+}
+
+int cl_graph_send_tokens_rank(cl_graph* g, int32_t src, int32_t dest, int64_t n) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  if (src < 0 || src >= g->n) return gerr(CL_E_UNKNOWN_NODE, "send from unknown rank %d", src);
+  return g->append_send(src, dest >= 0 && dest < g->n ? dest : -1, n);
+}
+
+int cl_graph_send_tokens(cl_graph* g, const char* src, const char* dest, int64_t n) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  const int32_t a = g->rank_of_id(src);
+  if (a < 0) return gerr(CL_E_UNKNOWN_NODE, "send from unknown node %s", src ? src : "(null)");
+  return g->append_send(a, g->rank_of_id(dest), n);  // unknown dest: fatal at run time (node.go:121-124)
+}
+
+int cl_graph_start_snapshot_rank(cl_graph* g, int32_t node, int32_t* out_sid) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  if (node < 0 || node >= g->n) return gerr(CL_E_UNKNOWN_NODE, "snapshot at unknown rank %d", node);
+  return g->append_snap(node, out_sid);
+}
+
+int cl_graph_start_snapshot(cl_graph* g, const char* node, int32_t* out_sid) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  const int32_t a = g->rank_of_id(node);
+  if (a < 0) return gerr(CL_E_UNKNOWN_NODE, "snapshot at unknown node %s", node ? node : "(null)");
+  return g->append_snap(a, out_sid);
+}
+
+int cl_graph_tick(cl_graph* g, int32_t n) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  return g->append_tick(n);
+}
+
+int cl_graph_drain(cl_graph* g) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  g->prog.push_back(ProgOp{P_DRAIN, 0, 0, 0});
+  return CL_OK;
+}
+
+int cl_graph_read_events_text(cl_graph* g, const char* text, int32_t* n_snapshots) {
+  G_CHECK(g);
+  if (!text) return gerr(CL_E_INVALID, "null text");
+  int32_t snaps = 0;
+  for (const std::string& line : go_lines(text)) {
+    if (line == "#") continue;  // strings.HasPrefix("#", line) (test_common.go:90, sic)
+    auto f = go_fields(line);
+    if (f.empty()) return gerr(CL_E_PARSE, "empty event line");
+    int rc;
+    if (f[0] == "send") {
+      int64_t nt;
+      if (f.size() < 4 || !go_atoi(f[3], &nt)) return gerr(CL_E_PARSE, "bad send line: %s", line.c_str());
+      rc = cl_graph_send_tokens(g, f[1].c_str(), f[2].c_str(), nt);
+    } else if (f[0] == "snapshot") {
+      if (f.size() < 2) return gerr(CL_E_PARSE, "bad snapshot line: %s", line.c_str());
+      snaps++;
+      rc = cl_graph_start_snapshot(g, f[1].c_str(), nullptr);
+    } else if (f[0] == "tick") {
+      int64_t nt = 1;
+      if (f.size() > 1 && !go_atoi(f[1], &nt)) return gerr(CL_E_PARSE, "bad tick line: %s", line.c_str());
+      if (nt > INT32_MAX) return gerr(CL_E_LIMIT, "tick count too large");
+      rc = cl_graph_tick(g, (int32_t)std::max<int64_t>(nt, 0));
+    } else {
+      return gerr(CL_E_PARSE, "Unknown event command: %s", f[0].c_str());
+    }
+    if (rc) return rc;
+  }
+  if (n_snapshots) *n_snapshots = snaps;
+  return cl_graph_drain(g);
+}
+
+int cl_graph_read_events_file(cl_graph* g, const char* path, int32_t* n_snapshots) {
+  G_CHECK(g);
+  std::string text;
+  if (!path || !read_file(path, &text)) return gerr(CL_E_IO, "cannot read %s", path ? path : "(null)");
+  return cl_graph_read_events_text(g, text.c_str(), n_snapshots);
+}
+
+int cl_graph_flush(cl_graph* g) {
+  G_CHECK(g);
+  return g->flush();
+}
+
+int cl_graph_rerun(cl_graph* g) {
+  G_CHECK(g);
+  return g->run(true);
+}
+
+int cl_graph_synchronize(cl_graph* g) {
+  G_CHECK(g);
+  return g->sync();
+}
+
+int cl_graph_run_time(cl_graph* g, double* total_ms, int64_t* runs, int64_t* ticks) {
+  G_CHECK(g);
+  if (!total_ms || !runs || !ticks) return gerr(CL_E_INVALID, "null output");
+  return g->fold_time(total_ms, runs, ticks);
+}
+
+int cl_graph_device_bytes(cl_graph* g, int64_t* bytes) {
+  G_CHECK(g);
+  if (!bytes) return gerr(CL_E_INVALID, "null output");
+  size_t b = 0;
+  b += g->d_out_off.bytes() + g->d_ch_dst.bytes() + g->d_ch_inpos.bytes() + g->d_in_off.bytes() +
+       g->d_in_src.bytes() + g->d_init_tok.bytes() + g->d_tokens.bytes() + g->d_pick.bytes() + g->d_trig.bytes() +
+       g->d_ltrig.bytes() + g->d_lsend.bytes() + g->d_crn.bytes() + g->d_mlist.bytes() + g->d_xl.bytes() +
+       g->d_mask.bytes() + g->d_cre.bytes() + g->d_bsum.bytes() + g->d_hc.bytes() + g->d_tokcnt.bytes() +
+       g->d_histv.bytes() + g->d_fifo.bytes() + g->d_deliv.bytes() + g->d_W.bytes() + g->d_rec.bytes() +
+       g->d_cnt.bytes() + g->d_stok.bytes() + g->d_done.bytes() + g->d_ctick.bytes() + g->d_sched.bytes();
+  *bytes = (int64_t)b;
+  return CL_OK;
+}
+
+int cl_graph_get_status(cl_graph* g, int32_t* status) {
+  G_CHECK(g);
+  if (!status) return gerr(CL_E_INVALID, "null output");
+  int rc = g->flush();
+  if (rc) return rc;
+  if ((rc = g->read_status(status))) return rc;
+  if (!*status && g->hang) *status = CL_INST_HANG;
+  return CL_OK;
+}
+
+int cl_graph_get_time(cl_graph* g, int64_t* time) {
+  G_CHECK(g);
+  if (!time) return gerr(CL_E_INVALID, "null output");
+  int rc = g->flush();
+  if (rc) return rc;
+  GScal sc;
+  GHIP(hipMemcpy(&sc, g->d_sc.p, sizeof sc, hipMemcpyDeviceToHost));
+  *time = sc.status ? sc.time : g->time;
+  return CL_OK;
+}
+
+int cl_graph_num_snapshots(cl_graph* g, int32_t* n) {
+  G_CHECK(g);
+  if (!n) return gerr(CL_E_INVALID, "null output");
+  *n = g->n_sids;
+  return CL_OK;
+}
+
+int cl_graph_node_tokens(cl_graph* g, int64_t* out) {
+  G_CHECK(g);
+  if (!out) return gerr(CL_E_INVALID, "null output");
+  int rc = g->flush();
+  if (rc) return rc;
+  std::vector<int32_t> t((size_t)g->n);
+  GHIP(hipMemcpy(t.data(), g->d_tokens.p, t.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < t.size(); ++i) out[i] = t[i];
+  return CL_OK;
+}
+
+int cl_graph_snapshot_tick(cl_graph* g, int32_t sid, int32_t* tick) {
+  G_CHECK(g);
+  if (!tick) return gerr(CL_E_INVALID, "null output");
+  if (sid < 0 || sid >= g->n_sids) return gerr(CL_E_INVALID, "unknown snapshot %d", sid);
+  int rc = g->flush();
+  if (rc) return rc;
+  GHIP(hipMemcpy(tick, g->d_ctick.p + sid, sizeof(int32_t), hipMemcpyDeviceToHost));
+  return CL_OK;
+}
+
+int cl_graph_collect_snapshot(cl_graph* g, int32_t sid, int64_t* tokens, int64_t* msg_offsets, int64_t* msg_tokens,
+                              int64_t msg_cap) {
+  G_CHECK(g);
+  if (sid < 0 || sid >= g->n_sids) return gerr(CL_E_INVALID, "unknown snapshot %d", sid);
+  int32_t tick;
+  int rc = cl_graph_snapshot_tick(g, sid, &tick);
+  if (rc) return rc;
+  if (tick < 0) return gerr(CL_E_NOT_COMPLETE, "snapshot %d has not completed", sid);
+  const size_t N = (size_t)g->n, E = (size_t)g->e;
+  if (tokens) {
+    std::vector<int32_t> st(N);
+    GHIP(hipMemcpy(st.data(), g->d_stok.p + (size_t)sid * N, N * sizeof(int32_t), hipMemcpyDeviceToHost));
+    for (size_t v = 0; v < N; ++v) tokens[v] = st[v];
+  }
+  if (!msg_offsets) return CL_OK;
+  std::vector<uint64_t> rec(E);
+  if (E) GHIP(hipMemcpy(rec.data(), g->d_rec.p + (size_t)sid * E, E * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  int64_t m = 0;
+  for (size_t c = 0; c < E; ++c) {
+    const uint64_t x = rec[g->ch_inpos[c]];
+    msg_offsets[c] = m;
+    m += (int64_t)((uint32_t)(x >> 32) - (uint32_t)x);
+  }
+  msg_offsets[E] = m;
+  if (m > msg_cap || (m > 0 && !msg_tokens)) return gerr(CL_E_LIMIT, "%lld messages exceed msg_cap", (long long)m);
+  std::vector<uint32_t> hv;
+  if (g->hist && m) {
+    hv.resize(E * (size_t)g->hist);
+    GHIP(hipMemcpy(hv.data(), g->d_histv.p, hv.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  for (size_t c = 0; c < E; ++c) {
+    const size_t k = (size_t)g->ch_inpos[c];
+    const uint64_t x = rec[k];
+    const uint32_t b = (uint32_t)x, e = (uint32_t)(x >> 32);
+    for (uint32_t q = b; q < e; ++q)
+      msg_tokens[msg_offsets[c] + (q - b)] = g->hist ? (int64_t)hv[k * g->hist + q] : 1;
+  }
+  return CL_OK;
+}
+
+int cl_graph_get_counters(cl_graph* g, int64_t* out) {
+  G_CHECK(g);
+  if (!out) return gerr(CL_E_INVALID, "null output");
+  int rc = g->flush();
+  if (rc) return rc;
+  GHIP(hipMemsetAsync(g->d_scratch.p, 0, sizeof(unsigned long long), g->stream));
+  if ((rc = g->k_err(cg_launch_finish(g->P, g->n_sids, g->d_scratch.p, g->stream)))) return rc;
+  GScal sc;
+  unsigned long long open = 0;
+  GHIP(hipMemcpyAsync(&sc, g->d_sc.p, sizeof sc, hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipMemcpyAsync(&open, g->d_scratch.p, sizeof open, hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  out[CL_CNT_PUSH] = (int64_t)sc.push;
+  out[CL_CNT_PEEK] = (int64_t)sc.peek;
+  out[CL_CNT_POP_TOKEN] = (int64_t)sc.pop_tok;
+  out[CL_CNT_POP_MARKER] = (int64_t)sc.pop_mk;
+  out[CL_CNT_RECORDED] = (int64_t)(sc.recorded + open);
+  out[CL_CNT_COMPLETED] = (int64_t)sc.completed;
+  out[CL_CNT_INSTANCES] = 1;
+  out[CL_CNT_TICKS] = sc.status ? sc.time : g->time;
+  return CL_OK;
+}
+
+int cl_graph_get_checksums(cl_graph* g, int64_t* out) {
+  G_CHECK(g);
+  if (!out) return gerr(CL_E_INVALID, "null output");
+  int rc = g->flush();
+  if (rc) return rc;
+  const size_t ns = 3 + (size_t)g->n_sids;
+  GHIP(hipMemsetAsync(g->d_scratch.p, 0, ns * sizeof(unsigned long long), g->stream));
+  if ((rc = g->k_err(cg_launch_checks(g->P, g->n_sids, g->d_scratch.p, g->stream)))) return rc;
+  std::vector<unsigned long long> r(ns);
+  std::vector<int32_t> ct((size_t)std::max(g->n_sids, 1));
+  GScal sc;
+  GHIP(hipMemcpyAsync(r.data(), g->d_scratch.p, ns * sizeof(unsigned long long), hipMemcpyDeviceToHost, g->stream));
+  if (g->n_sids)
+    GHIP(hipMemcpyAsync(ct.data(), g->d_ctick.p, (size_t)g->n_sids * sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipMemcpyAsync(&sc, g->d_sc.p, sizeof sc, hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  int64_t cut = 0, completed = 0;
+  for (int32_t s = 0; s < g->n_sids; ++s) {
+    if (ct[s] < 0) continue;
+    completed++;
+    const int64_t d = (int64_t)r[3 + s] - g->total_tokens;
+    cut += d < 0 ? -d : d;
+  }
+  const int64_t fin = (int64_t)r[0] + (int64_t)r[1] - g->total_tokens;
+  out[CL_GSUM_OK] = (sc.status == 0 && !g->hang) ? 1 : 0;
+  out[CL_GSUM_DELIVERED] = (int64_t)(sc.pop_tok + sc.pop_mk);
+  out[CL_GSUM_COMPLETED] = completed;
+  out[CL_GSUM_CUT_RESIDUAL] = cut;
+  out[CL_GSUM_FINAL_RESIDUAL] = fin < 0 ? -fin : fin;
+  out[CL_GSUM_DIGEST] = (int64_t)r[2];
+  out[CL_GSUM_IN_FLIGHT] = (int64_t)r[1];
+  return CL_OK;
+}
+
+}  // extern "C"

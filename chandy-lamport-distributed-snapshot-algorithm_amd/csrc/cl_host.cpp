@@ -26,8 +26,22 @@
 
 #include "../../include/clsnap.h"
 #include "cl_engine.h"
+#include "cl_text.h"
 
 using namespace clsnap;
+
+namespace clsnap {
+namespace {
+thread_local std::string g_last_error;
+}
+int set_error_v(int code, const char* fmt, va_list ap) {
+  char buf[512];
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  g_last_error = buf;
+  return code;
+}
+const char* last_error() { return g_last_error.c_str(); }
+}  // namespace clsnap
 
 // Per-wave LDS words available for staging the wave's delay rows (kernel reads the
 // delays from LDS instead of HBM when ipw * row fits).
@@ -37,16 +51,12 @@ constexpr int32_t kTargetBlocks = 4;
 
 namespace {
 
-thread_local std::string g_last_error;
-
 int set_err(int code, const char* fmt, ...) {
-  char buf[512];
   va_list ap;
   va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
+  const int rc = set_error_v(code, fmt, ap);
   va_end(ap);
-  g_last_error = buf;
-  return code;
+  return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -120,61 +130,6 @@ void go_schedule(int64_t seed_base, int64_t n, int64_t draws, uint8_t* out) {
     });
   }
   for (auto& x : th) x.join();
-}
-
-// ---------------------------------------------------------------------------
-// Go-style text helpers (strings.Fields, strconv.Atoi, FieldsFunc(s, '\n'))
-// ---------------------------------------------------------------------------
-bool go_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
-
-std::vector<std::string> go_fields(const std::string& s) {
-  std::vector<std::string> f;
-  size_t i = 0;
-  while (i < s.size()) {
-    while (i < s.size() && go_space(s[i])) ++i;
-    if (i >= s.size()) break;
-    size_t j = i;
-    while (j < s.size() && !go_space(s[j])) ++j;
-    f.emplace_back(s.substr(i, j - i));
-    i = j;
-  }
-  return f;
-}
-
-bool go_atoi(const std::string& s, int64_t* out) {
-  size_t i = 0;
-  bool neg = false;
-  if (i < s.size() && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
-  if (i >= s.size()) return false;
-  int64_t v = 0;
-  for (; i < s.size(); ++i) {
-    if (s[i] < '0' || s[i] > '9') return false;
-    if (v > (INT64_MAX - (s[i] - '0')) / 10) return false;
-    v = v * 10 + (s[i] - '0');
-  }
-  *out = neg ? -v : v;
-  return true;
-}
-
-std::vector<std::string> go_lines(const std::string& s) {
-  std::vector<std::string> out;
-  size_t i = 0;
-  while (i <= s.size()) {
-    size_t j = s.find('\n', i);
-    if (j == std::string::npos) j = s.size();
-    if (j > i) out.emplace_back(s.substr(i, j - i));
-    i = j + 1;
-  }
-  return out;
-}
-
-bool read_file(const char* path, std::string* out) {
-  std::ifstream f(path, std::ios::binary);
-  if (!f) return false;
-  std::ostringstream ss;
-  ss << f.rdbuf();
-  *out = ss.str();
-  return true;
 }
 
 #define HIP_TRY(expr)                                                                     \
@@ -637,7 +592,7 @@ struct cl_sim {
 // ---------------------------------------------------------------------------
 extern "C" {
 
-const char* cl_last_error(void) { return g_last_error.c_str(); }
+const char* cl_last_error(void) { return last_error(); }
 
 const char* cl_status_string(int32_t code) {
   switch (code) {
@@ -647,6 +602,7 @@ const char* cl_status_string(int32_t code) {
     case CL_INST_FIFO_OVERFLOW: return "fifo overflow (engine limit)";
     case CL_INST_HANG: return "hang: snapshot never completed";
     case CL_INST_DELAY_EXHAUSTED: return "delay schedule exhausted";
+    case CL_INST_HIST_OVERFLOW: return "token history overflow (engine limit)";
     default: return "unknown";
   }
 }

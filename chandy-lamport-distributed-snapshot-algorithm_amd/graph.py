@@ -1,0 +1,289 @@
+"""Graph engine: ONE reference simulation over a large topology (include/clgraph.h).
+
+``GraphSim`` mirrors the reference simulator API (sim.go ``ChandyLamportSim``:
+``AddNode``, ``AddLink``, ``ProcessEvent``, ``Tick``, ``StartSnapshot``,
+``CollectSnapshot``) for a single run whose nodes and channels span the whole GPU --
+BASELINE configs 4 (2^20-node random regular digraph under continuous token traffic)
+and 5 (100k-node power-law graph with 4,096 overlapping snapshots) -- and runs the
+reference's own test_data scenarios as well.  There is no CPU fallback: without the
+HIP library or a gfx950 GPU, calls that need them raise ``ClSnapError``.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import (ClSnapError, GlobalSnapshot, MsgSnapshot, PassTokenEvent, SnapshotEvent, _check, _p,
+               COUNTER_NAMES, lib)
+
+GSUM_NAMES = ("ok", "delivered", "completed", "cut_residual", "final_residual", "digest", "in_flight")
+
+_SIGS = None
+
+
+def glib():
+    """The engine library with the cl_graph_* signatures bound."""
+    global _SIGS
+    L = lib()
+    if _SIGS is None:
+        vp, i64, i32, u64, u32, cp = C.c_void_p, C.c_int64, C.c_int32, C.c_uint64, C.c_uint32, C.c_char_p
+        sig = {
+            "cl_graph_create": [C.POINTER(C.c_void_p)],
+            "cl_graph_destroy": [vp],
+            "cl_graph_set_device": [vp, i32],
+            "cl_graph_add_node": [vp, cp, i64],
+            "cl_graph_add_link": [vp, cp, cp],
+            "cl_graph_read_topology_text": [vp, cp],
+            "cl_graph_read_topology_file": [vp, cp],
+            "cl_graph_set_topology": [vp, i32, i32, vp, i64, vp, vp],
+            "cl_graph_generate_regular": [vp, i32, i32, i64, u64],
+            "cl_graph_generate_powerlaw": [vp, i32, i32, C.c_double, i32, i64, u64],
+            "cl_graph_num_nodes": [vp, vp],
+            "cl_graph_num_channels": [vp, vp],
+            "cl_graph_channels": [vp, vp, vp],
+            "cl_graph_node_id": [vp, i32, vp, i32],
+            "cl_graph_set_limits": [vp, i32, i32, i64],
+            "cl_graph_set_delay_hash": [vp, u64],
+            "cl_graph_set_delay_go_seed": [vp, i64],
+            "cl_graph_set_delay_schedule": [vp, vp, i64],
+            "cl_graph_set_traffic": [vp, u64, u32, i64],
+            "cl_graph_send_tokens": [vp, cp, cp, i64],
+            "cl_graph_send_tokens_rank": [vp, i32, i32, i64],
+            "cl_graph_start_snapshot": [vp, cp, vp],
+            "cl_graph_start_snapshot_rank": [vp, i32, vp],
+            "cl_graph_tick": [vp, i32],
+            "cl_graph_drain": [vp],
+            "cl_graph_read_events_text": [vp, cp, vp],
+            "cl_graph_read_events_file": [vp, cp, vp],
+            "cl_graph_flush": [vp],
+            "cl_graph_rerun": [vp],
+            "cl_graph_synchronize": [vp],
+            "cl_graph_run_time": [vp, vp, vp, vp],
+            "cl_graph_device_bytes": [vp, vp],
+            "cl_graph_get_status": [vp, vp],
+            "cl_graph_get_time": [vp, vp],
+            "cl_graph_num_snapshots": [vp, vp],
+            "cl_graph_node_tokens": [vp, vp],
+            "cl_graph_snapshot_tick": [vp, i32, vp],
+            "cl_graph_collect_snapshot": [vp, i32, vp, vp, vp, i64],
+            "cl_graph_get_counters": [vp, vp],
+            "cl_graph_get_checksums": [vp, vp],
+        }
+        for name, args in sig.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = C.c_int, args
+        L.cl_counter_hash.restype, L.cl_counter_hash.argtypes = u64, [u64, u64, u64]
+        _SIGS = sig
+    return L
+
+
+def counter_hash(seed, a, b):
+    """The synthetic workloads' counter hash (cg_hash, cg_engine.h)."""
+    return glib().cl_counter_hash(seed, a, b)
+
+
+class GraphSim:
+    """One reference simulator (sim.go ChandyLamportSim) on the GPU, state in HBM."""
+
+    def __init__(self, device=0, fifo_slots=16, max_snapshots=0, max_drain_ticks=10000):
+        self._L = glib()
+        h = C.c_void_p()
+        _check(self._L.cl_graph_create(C.byref(h)))
+        self._h = h
+        _check(self._L.cl_graph_set_device(self._h, device))
+        _check(self._L.cl_graph_set_limits(self._h, fifo_slots, max_snapshots, max_drain_ticks))
+        self._ids = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.cl_graph_destroy(h)
+            self._h = None
+
+    # ---- topology -----------------------------------------------------------------
+    def AddNode(self, node_id, tokens):             # sim.go:40
+        _check(self._L.cl_graph_add_node(self._h, node_id.encode(), tokens))
+
+    def AddLink(self, src, dest):                   # sim.go:46
+        _check(self._L.cl_graph_add_link(self._h, src.encode(), dest.encode()))
+
+    def read_topology_file(self, path):             # test_common.go:29
+        _check(self._L.cl_graph_read_topology_file(self._h, path.encode()))
+
+    def read_topology_text(self, text):
+        _check(self._L.cl_graph_read_topology_text(self._h, text.encode()))
+
+    def set_topology(self, tokens, src, dst, id_width=0):
+        tok = np.ascontiguousarray(tokens, dtype=np.int64)
+        s = np.ascontiguousarray(src, dtype=np.int32)
+        d = np.ascontiguousarray(dst, dtype=np.int32)
+        _check(self._L.cl_graph_set_topology(self._h, tok.size, id_width, _p(tok), s.size, _p(s), _p(d)))
+
+    def generate_regular(self, n_nodes, degree=8, tokens=100, seed=0):
+        _check(self._L.cl_graph_generate_regular(self._h, n_nodes, degree, tokens, seed))
+
+    def generate_powerlaw(self, n_nodes, targets=8, exponent=0.9, ring=True, tokens=100, seed=0):
+        _check(self._L.cl_graph_generate_powerlaw(self._h, n_nodes, targets, exponent, 1 if ring else 0,
+                                                  tokens, seed))
+
+    # ---- configuration --------------------------------------------------------------
+    def set_limits(self, fifo_slots=16, max_snapshots=0, max_drain_ticks=10000):
+        _check(self._L.cl_graph_set_limits(self._h, fifo_slots, max_snapshots, max_drain_ticks))
+
+    def set_delay_hash(self, seed):
+        _check(self._L.cl_graph_set_delay_hash(self._h, seed))
+
+    def set_delay_go_seed(self, seed):
+        _check(self._L.cl_graph_set_delay_go_seed(self._h, seed))
+
+    def set_delay_schedule(self, delays):
+        d = np.ascontiguousarray(delays, dtype=np.uint8).ravel()
+        _check(self._L.cl_graph_set_delay_schedule(self._h, _p(d), d.size))
+
+    def set_traffic(self, seed, threshold, steps):
+        _check(self._L.cl_graph_set_traffic(self._h, seed, threshold, steps))
+
+    # ---- events -------------------------------------------------------------------------
+    def ProcessEvent(self, event):                  # sim.go:58
+        if isinstance(event, PassTokenEvent):
+            _check(self._L.cl_graph_send_tokens(self._h, event.src.encode(), event.dest.encode(), event.tokens))
+        elif isinstance(event, SnapshotEvent):
+            self.StartSnapshot(event.nodeId)
+        else:
+            raise ClSnapError(-1, f"Error unknown event: {event!r}")
+
+    def send_tokens_rank(self, src, dest, n):
+        _check(self._L.cl_graph_send_tokens_rank(self._h, src, dest, n))
+
+    def Tick(self, n=1):                            # sim.go:71
+        _check(self._L.cl_graph_tick(self._h, n))
+
+    def StartSnapshot(self, node_id):               # sim.go:105
+        sid = C.c_int32(-1)
+        _check(self._L.cl_graph_start_snapshot(self._h, node_id.encode(), C.byref(sid)))
+        return sid.value
+
+    def start_snapshot_rank(self, rank):
+        sid = C.c_int32(-1)
+        _check(self._L.cl_graph_start_snapshot_rank(self._h, rank, C.byref(sid)))
+        return sid.value
+
+    def drain(self):                                # test_common.go:123-137
+        _check(self._L.cl_graph_drain(self._h))
+
+    def read_events_file(self, path):               # test_common.go:79 (incl. drain)
+        n = C.c_int32(0)
+        _check(self._L.cl_graph_read_events_file(self._h, path.encode(), C.byref(n)))
+        return n.value
+
+    def read_events_text(self, text):
+        n = C.c_int32(0)
+        _check(self._L.cl_graph_read_events_text(self._h, text.encode(), C.byref(n)))
+        return n.value
+
+    # ---- execution ----------------------------------------------------------------------
+    def flush(self):
+        _check(self._L.cl_graph_flush(self._h))
+
+    def rerun(self):
+        _check(self._L.cl_graph_rerun(self._h))
+
+    def synchronize(self):
+        _check(self._L.cl_graph_synchronize(self._h))
+
+    def run_time(self):
+        """(device ms of the runs since the previous call, runs, ticks) -- HIP events."""
+        ms, r, t = C.c_double(0), C.c_int64(0), C.c_int64(0)
+        _check(self._L.cl_graph_run_time(self._h, C.byref(ms), C.byref(r), C.byref(t)))
+        return ms.value, r.value, t.value
+
+    # ---- queries ------------------------------------------------------------------------
+    def _get(self, fn, ctype, *args):
+        v = ctype(0)
+        _check(fn(self._h, *args, C.byref(v)))
+        return v.value
+
+    @property
+    def num_nodes(self):
+        return self._get(self._L.cl_graph_num_nodes, C.c_int32)
+
+    @property
+    def num_channels(self):
+        return self._get(self._L.cl_graph_num_channels, C.c_int64)
+
+    @property
+    def num_snapshots(self):
+        return self._get(self._L.cl_graph_num_snapshots, C.c_int32)
+
+    @property
+    def device_bytes(self):
+        return self._get(self._L.cl_graph_device_bytes, C.c_int64)
+
+    def channels(self):
+        e = self.num_channels
+        s = np.zeros(e, dtype=np.int32)
+        d = np.zeros(e, dtype=np.int32)
+        _check(self._L.cl_graph_channels(self._h, _p(s), _p(d)))
+        return s, d
+
+    def node_ids(self):
+        if self._ids is None:
+            buf = C.create_string_buffer(64)
+            out = []
+            for r in range(self.num_nodes):
+                _check(self._L.cl_graph_node_id(self._h, r, buf, 64))
+                out.append(buf.value.decode())
+            self._ids = out
+        return self._ids
+
+    def status(self):
+        return self._get(self._L.cl_graph_get_status, C.c_int32)
+
+    def time(self):
+        return self._get(self._L.cl_graph_get_time, C.c_int64)
+
+    def node_tokens_array(self):
+        out = np.zeros(self.num_nodes, dtype=np.int64)
+        _check(self._L.cl_graph_node_tokens(self._h, _p(out)))
+        return out
+
+    def node_tokens(self):
+        return dict(zip(self.node_ids(), self.node_tokens_array().tolist()))
+
+    def snapshot_tick(self, sid):
+        return self._get(self._L.cl_graph_snapshot_tick, C.c_int32, sid)
+
+    def collect_arrays(self, sid):
+        """(tokens[N] rank order, offsets[E+1], messages) with channels in (src, dest)
+        rank order; raises ClSnapError(-9) if the snapshot has not completed."""
+        n, e = self.num_nodes, self.num_channels
+        tok = np.zeros(n, dtype=np.int64)
+        off = np.zeros(e + 1, dtype=np.int64)
+        cap = 1 << 16
+        while True:
+            msg = np.zeros(cap, dtype=np.int64)
+            rc = self._L.cl_graph_collect_snapshot(self._h, sid, _p(tok), _p(off), _p(msg), cap)
+            if rc == -7 and off[e] > cap:
+                cap = int(off[e])
+                continue
+            _check(rc)
+            return tok, off, msg[:off[e]]
+
+    def CollectSnapshot(self, snapshot_id):         # sim.go:134
+        """GlobalSnapshot, messages in (dest, src, delivery) order."""
+        tok, off, msg = self.collect_arrays(snapshot_id)
+        ids = self.node_ids()
+        src, dst = self.channels()
+        order = np.lexsort((src, dst))
+        msgs = [MsgSnapshot(ids[src[c]], ids[dst[c]], int(msg[k]))
+                for c in order for k in range(off[c], off[c + 1])]
+        return GlobalSnapshot(snapshot_id, dict(zip(ids, tok.tolist())), msgs)
+
+    def counters(self):
+        out = np.zeros(len(COUNTER_NAMES), dtype=np.int64)
+        _check(self._L.cl_graph_get_counters(self._h, _p(out)))
+        return dict(zip(COUNTER_NAMES, out.tolist()))
+
+    def checksums(self):
+        out = np.zeros(len(GSUM_NAMES), dtype=np.int64)
+        _check(self._L.cl_graph_get_checksums(self._h, _p(out)))
+        return dict(zip(GSUM_NAMES, out.tolist()))

@@ -1,0 +1,144 @@
+/*
+ * clgraph.h -- C ABI of the MI355X graph engine: ONE reference Chandy-Lamport
+ * simulation (sim.go ChandyLamportSim) over a large topology, state in HBM.
+ *
+ * Where clsnap.h batches many copies of a small scenario (one wave segment per
+ * instance), cl_graph runs a single instance whose nodes and channels span the whole
+ * GPU: BASELINE configs 4 (2^20-node random 8-out-regular digraph, one snapshot under
+ * continuous token traffic) and 5 (100k-node power-law graph, 4,096 overlapping
+ * snapshots).  It keeps the reference's semantics bit-exactly -- tick order, same-tick
+ * visibility, the global delay-draw order, per-channel recording -- and runs the
+ * reference's test_data scenarios too (parity-tested against the golden snapshots).
+ *
+ * Conventions follow clsnap.h: int return codes (CL_OK / CL_E_*), cl_last_error(),
+ * caller-allocated buffers, one host thread per cl_graph, node order = getSortedKeys
+ * (common.go:135-146) rank, channel c = the c-th link in (src rank, dest rank) order.
+ * Per-run fatal conditions become a status (CL_INST_*) and freeze the simulation.
+ *
+ * Event model.  The engine executes a program of steps; step k (simulator time k) is:
+ *   1. synthetic traffic sends of step k (if configured, cl_graph_set_traffic),
+ *   2. host events (cl_graph_send_tokens / cl_graph_start_snapshot) in call order,
+ *   3. one Tick (sim.go:71-95).
+ * Host calls only append to the program; cl_graph_flush() executes what is pending
+ * on the GPU, and cl_graph_rerun() replays the whole program from the initial state.
+ */
+#ifndef CLGRAPH_H
+#define CLGRAPH_H
+
+#include <stdint.h>
+
+#include "clsnap.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- checksums (cl_graph_get_checksums), int64, all-reducible across ranks ---- */
+#define CL_GSUM_OK 0             /* 1 if the run's status is CL_INST_OK */
+#define CL_GSUM_DELIVERED 1      /* delivered packets (sim.go:85 pops) */
+#define CL_GSUM_COMPLETED 2      /* globally completed snapshots */
+#define CL_GSUM_CUT_RESIDUAL 3   /* sum over completed snapshots |tokens + recorded - total| */
+#define CL_GSUM_FINAL_RESIDUAL 4 /* |final tokens + in-flight tokens - total| (checkTokens) */
+#define CL_GSUM_DIGEST 5         /* sum of per-snapshot content digests */
+#define CL_GSUM_IN_FLIGHT 6      /* token payloads still queued */
+#define CL_NUM_GSUMS 7
+
+typedef struct cl_graph cl_graph;
+
+int cl_graph_create(cl_graph** out);
+int cl_graph_destroy(cl_graph* g);
+int cl_graph_set_device(cl_graph* g, int32_t device_ordinal);
+
+/* ---- topology (before the first event) ------------------------------------- */
+/* AddNode / AddLink (sim.go:40-56; node.go:45-55,87-94) and readTopologyFile
+ * (test_common.go:29-68): string ids, ranked by lexicographic order at freeze. */
+int cl_graph_add_node(cl_graph* g, const char* id, int64_t tokens);
+int cl_graph_add_link(cl_graph* g, const char* src, const char* dest);
+int cl_graph_read_topology_text(cl_graph* g, const char* text);
+int cl_graph_read_topology_file(cl_graph* g, const char* path);
+/* Bulk topology by rank: node r is "N" + r zero-padded to id_width digits (so rank ==
+ * lexicographic order; id_width = 0 picks the digits of n_nodes-1), tokens[r]; the
+ * links AddLink(src[i], dst[i]) with self links ignored and duplicates collapsed. */
+int cl_graph_set_topology(cl_graph* g, int32_t n_nodes, int32_t id_width, const int64_t* tokens,
+                          int64_t n_edges, const int32_t* src, const int32_t* dst);
+/* Synthetic graphs:
+ * regular: `degree` random permutations pi_p (Fisher-Yates driven by
+ *   cl_counter_hash(seed, p, i)), links v -> pi_p(v);
+ * powerlaw: `targets` links per node to ranks drawn from Zipf(exponent) over rank,
+ *   plus ring links v -> v+1 and v -> v-1 when ring != 0.
+ * Every node starts with `tokens` tokens. */
+int cl_graph_generate_regular(cl_graph* g, int32_t n_nodes, int32_t degree, int64_t tokens, uint64_t seed);
+int cl_graph_generate_powerlaw(cl_graph* g, int32_t n_nodes, int32_t targets, double exponent, int32_t ring,
+                               int64_t tokens, uint64_t seed);
+
+int cl_graph_num_nodes(cl_graph* g, int32_t* n);
+int cl_graph_num_channels(cl_graph* g, int64_t* n);
+/* src[c], dst[c] ranks of every channel, channel order */
+int cl_graph_channels(cl_graph* g, int32_t* src, int32_t* dst);
+/* node id of a rank, NUL-terminated into buf[cap] */
+int cl_graph_node_id(cl_graph* g, int32_t rank, char* buf, int32_t cap);
+
+/* ---- configuration (before the first flush) -------------------------------- */
+/* fifo_slots: ring slots per channel (power of two, 2..32768; deeper -> FIFO_OVERFLOW
+ * status); max_snapshots: snapshot ids provisioned (0 = the program's count, at least
+ * 16); max_drain_ticks bounds cl_graph_drain (HANG status). */
+int cl_graph_set_limits(cl_graph* g, int32_t fifo_slots, int32_t max_snapshots, int64_t max_drain_ticks);
+/* Delay source replacing rand.Intn(maxDelay) at sim.go:101; draw k of the run gets
+ *   hash:     (cl_counter_hash(seed, k, 0) >> 32) % 5          (default, seed 0)
+ *   go seed:  the k-th rand.Intn(5) of rand.Seed(seed)          (snapshot_test.go:20)
+ *   schedule: delays[k] (values in [0, 5); DELAY_EXHAUSTED beyond n). */
+int cl_graph_set_delay_hash(cl_graph* g, uint64_t seed);
+int cl_graph_set_delay_go_seed(cl_graph* g, int64_t seed);
+int cl_graph_set_delay_schedule(cl_graph* g, const uint8_t* delays, int64_t n);
+/* Synthetic traffic: at every step k < steps, each node (rank order) holding tokens
+ * with out-links sends ONE token when (uint32)cl_counter_hash(seed, k, rank) <
+ * threshold, on out-link ((hash >> 32) * outdeg) >> 32 (SendTokens node.go:112-131). */
+int cl_graph_set_traffic(cl_graph* g, uint64_t seed, uint32_t threshold, int64_t steps);
+
+/* ---- events ------------------------------------------------------------------ */
+int cl_graph_send_tokens(cl_graph* g, const char* src, const char* dest, int64_t n);  /* sim.go:58-62 */
+int cl_graph_send_tokens_rank(cl_graph* g, int32_t src, int32_t dest, int64_t n);
+int cl_graph_start_snapshot(cl_graph* g, const char* node, int32_t* out_sid);         /* sim.go:105 */
+int cl_graph_start_snapshot_rank(cl_graph* g, int32_t node, int32_t* out_sid);
+int cl_graph_tick(cl_graph* g, int32_t n);                                             /* sim.go:71 */
+/* test_common.go:123-137: tick until every started snapshot completed, then
+ * maxDelay+1 more ticks.  Host-driven (checks completion between ticks). */
+int cl_graph_drain(cl_graph* g);
+int cl_graph_read_events_text(cl_graph* g, const char* text, int32_t* n_snapshots); /* test_common.go:79-140 */
+int cl_graph_read_events_file(cl_graph* g, const char* path, int32_t* n_snapshots);
+
+/* ---- execution ---------------------------------------------------------------- */
+int cl_graph_flush(cl_graph* g);
+/* Reset to the initial topology state and replay the whole program, asynchronously
+ * when it has no drain (the benchmark step); cl_graph_synchronize() waits. */
+int cl_graph_rerun(cl_graph* g);
+int cl_graph_synchronize(cl_graph* g);
+/* Device time of the runs since the previous call (HIP events on the engine stream
+ * around each flush / rerun), the number of runs, and the ticks they executed. */
+int cl_graph_run_time(cl_graph* g, double* total_ms, int64_t* runs, int64_t* ticks);
+int cl_graph_device_bytes(cl_graph* g, int64_t* bytes);
+
+/* ---- results (flush pending events first) ----------------------------------- */
+int cl_graph_get_status(cl_graph* g, int32_t* status);
+int cl_graph_get_time(cl_graph* g, int64_t* time);
+int cl_graph_num_snapshots(cl_graph* g, int32_t* n);
+int cl_graph_node_tokens(cl_graph* g, int64_t* out /* [num_nodes] */);
+int cl_graph_snapshot_tick(cl_graph* g, int32_t sid, int32_t* tick);
+/* CollectSnapshot (sim.go:134-173): tokens[rank] = tokenMap; the messages recorded on
+ * channel c are msg_tokens[msg_offsets[c] .. msg_offsets[c+1]) in delivery order.
+ * CL_E_NOT_COMPLETE if sid has not completed; CL_E_LIMIT (offsets written) if msg_cap
+ * is too small. */
+int cl_graph_collect_snapshot(cl_graph* g, int32_t sid, int64_t* tokens, int64_t* msg_offsets,
+                              int64_t* msg_tokens, int64_t msg_cap);
+/* CL_CNT_* counters (clsnap.h) of the run; recorded copies include channels still
+ * recording at the end. */
+int cl_graph_get_counters(cl_graph* g, int64_t* out /* [CL_NUM_COUNTERS] */);
+int cl_graph_get_checksums(cl_graph* g, int64_t* out /* [CL_NUM_GSUMS] */);
+
+/* ---- counter hash of the synthetic workloads ------------------------------------ */
+uint64_t cl_counter_hash(uint64_t seed, uint64_t a, uint64_t b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLGRAPH_H */

@@ -56,6 +56,7 @@ extern "C" {
 #define CL_INST_FIFO_OVERFLOW 3             /* engine: channel deeper than 255 packets */
 #define CL_INST_HANG 4                      /* drain exceeded max ticks (test_common.go:124-132 loops forever) */
 #define CL_INST_DELAY_EXHAUSTED 5           /* replayed delay schedule too short */
+#define CL_INST_HIST_OVERFLOW 6             /* graph engine: token history slots exhausted */
 
 /* ---- counters (cl_get_counters), summed over instances ------------------ */
 #define CL_CNT_PUSH 0      /* Queue.Push (queue.go:18) == delay draws (sim.go:101) */

@@ -198,6 +198,8 @@ typedef struct orc_sim {
     int status;
     /* delay source */
     int use_go;
+    int use_hash;              /* counter-hash delays (synthetic workloads) */
+    uint64_t hash_seed;
     go_rng rng;
     const uint8_t* sched;
     int64_t sched_len, sched_pos;
@@ -242,12 +244,36 @@ void orc_free(orc_sim* s) {
     free(s);
 }
 
-void orc_seed_go(orc_sim* s, int64_t seed) { s->use_go = 1; go_rng_seed(&s->rng, seed); }
+void orc_seed_go(orc_sim* s, int64_t seed) { s->use_go = 1; s->use_hash = 0; go_rng_seed(&s->rng, seed); }
+
+/* ------------------------------------------------------------------------- */
+/* Counter hash for the synthetic workloads.  Same     */
+/* definition as the engine's cg_hash (csrc/cg_engine.h), restated here so the */
+/* two are checked against each other rather than shared.                      */
+/* ------------------------------------------------------------------------- */
+static uint64_t mix64(uint64_t z);
+
+uint64_t orc_counter_hash(uint64_t seed, uint64_t a, uint64_t b) {
+    uint64_t h = mix64(seed ^ (a * 0x9E3779B97F4A7C15ULL));
+    return mix64(h ^ (b * 0xD6E8FEB86659FD93ULL));
+}
+
+/* Delay of draw k under the counter-hash source: replaces rand.Intn(maxDelay) at
+ * sim.go:101 by a pure function of the instance's draw index, so the reference's
+ * draw ORDER (host events in order, then deliveries in sender order) still decides
+ * every delay. */
+int orc_counter_delay(uint64_t seed, uint64_t k) {
+    return (int)((orc_counter_hash(seed, k, 0) >> 32) % 5u);
+}
+
+void orc_use_counter_hash(orc_sim* s, uint64_t seed) {
+    s->use_go = 0; s->use_hash = 1; s->hash_seed = seed;
+}
 
 /* Replay a per-message delay schedule (values in [0, MAX_DELAY)). The caller keeps
  * the buffer alive. This replaces rand.Intn(maxDelay) at sim.go:101. */
 void orc_use_schedule(orc_sim* s, const uint8_t* delays, int64_t len) {
-    s->use_go = 0; s->sched = delays; s->sched_len = len; s->sched_pos = 0;
+    s->use_go = 0; s->use_hash = 0; s->sched = delays; s->sched_len = len; s->sched_pos = 0;
 }
 
 int orc_status(const orc_sim* s) { return s->status; }
@@ -369,6 +395,8 @@ static int get_receive_time(orc_sim* s, int64_t* rt) {
     int d;
     if (s->use_go) {
         d = go_intn(&s->rng, MAX_DELAY);
+    } else if (s->use_hash) {
+        d = orc_counter_delay(s->hash_seed, (uint64_t)s->cnt.draws);
     } else {
         if (s->sched_pos >= s->sched_len) return ORC_DELAY_EXHAUSTED;
         d = s->sched[s->sched_pos++];
@@ -520,15 +548,11 @@ int orc_tick(orc_sim* s) {
     return ORC_OK;
 }
 
-/* node.go:112-131 SendTokens (via sim.go:58-62 ProcessEvent) */
-int orc_send_tokens(orc_sim* s, const char* src, const char* dest, int64_t num) {
-    if (s->status) return s->status;
-    int a = find_node(s, src);
-    if (a < 0) return ORC_ERR_API; /* nil *Node dereference in the reference */
+/* node.go:112-131 SendTokens (via sim.go:58-62 ProcessEvent); a, b node indices */
+static int send_tokens_idx(orc_sim* s, int a, int b, int64_t num) {
     orc_node* n = &s->nodes[a];
     if (n->tokens < num) { s->status = ORC_FATAL_INSUFFICIENT_TOKENS; return s->status; }
     n->tokens -= num;
-    int b = find_node(s, dest);
     orc_link* l = NULL;
     for (int k = 0; k < n->n_out && b >= 0; k++)
         if (s->links[n->out_links[k]].dest == b) l = &s->links[n->out_links[k]];
@@ -540,6 +564,23 @@ int orc_send_tokens(orc_sim* s, const char* src, const char* dest, int64_t num) 
     queue_push(&l->q, e);
     s->cnt.push++;
     return ORC_OK;
+}
+
+int orc_send_tokens(orc_sim* s, const char* src, const char* dest, int64_t num) {
+    if (s->status) return s->status;
+    int a = find_node(s, src);
+    if (a < 0) return ORC_ERR_API; /* nil *Node dereference in the reference */
+    return send_tokens_idx(s, a, find_node(s, dest), num);
+}
+
+/* sim.go:105-123 StartSnapshot on node index a */
+static int start_snapshot_idx(orc_sim* s, int a, int* out_sid) {
+    int sid = s->next_snapshot_id++;
+    ensure_sids(s, sid);
+    if (out_sid) *out_sid = sid;
+    int rc = node_start_snapshot(s, a, sid);
+    if (rc) s->status = rc;
+    return rc;
 }
 
 /* sim.go:105-123 StartSnapshot */
@@ -861,4 +902,131 @@ double orc_run_batch(const char* top_text, const char* events_text, int64_t n,
     free(jobs); free(th);
     if (err) return -1.0;
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic large-graph driver         */
+/* ------------------------------------------------------------------------- */
+/* Build a topology from ranks: node r gets id "N" + r zero-padded to `width`
+ * digits (lexicographic order == numeric order, so rank r is sorted position r),
+ * then AddLink(src[i], dst[i]) in edge order -- the same calls readTopologyFile
+ * would make (test_common.go:29-68), without re-sorting after every AddNode. */
+int orc_build_graph(orc_sim* s, int n, const int64_t* tokens, int64_t m, const int32_t* src,
+                    const int32_t* dst, int width) {
+    if (s->n_nodes) return ORC_ERR_API;
+    s->nodes = (orc_node*)xrealloc(s->nodes, sizeof(orc_node) * (size_t)(n ? n : 1));
+    s->cap_nodes = n ? n : 1;
+    char buf[32];
+    for (int r = 0; r < n; r++) {
+        orc_node* nd = &s->nodes[r];
+        memset(nd, 0, sizeof(*nd));
+        snprintf(buf, sizeof buf, "N%0*d", width, r);
+        nd->id = strdup(buf);
+        nd->tokens = tokens[r];
+    }
+    s->n_nodes = n;
+    resort(s);
+    for (int r = 0; r < n; r++)
+        if (s->sorted[r] != r) return ORC_ERR_API; /* width too small for lexicographic == numeric */
+    for (int64_t i = 0; i < m; i++) {
+        int a = src[i], b = dst[i];
+        if (a < 0 || b < 0 || a >= n || b >= n) return ORC_ERR_API;
+        if (a == b) continue; /* node.go:88-90 */
+        orc_node* na = &s->nodes[a];
+        int dup = 0;
+        for (int k = 0; k < na->n_out && !dup; k++) dup = s->links[na->out_links[k]].dest == b;
+        if (dup) continue; /* map assignment: a fresh queue, nothing pushed yet */
+        if (s->n_links == s->cap_links) {
+            s->cap_links = s->cap_links ? 2 * s->cap_links : 16;
+            s->links = (orc_link*)xrealloc(s->links, sizeof(orc_link) * (size_t)s->cap_links);
+        }
+        int li = s->n_links++;
+        memset(&s->links[li], 0, sizeof(orc_link));
+        s->links[li].src = a;
+        s->links[li].dest = b;
+        insert_sorted(s, &na->out_links, &na->n_out, &na->cap_out, li, 1);
+        orc_node* nb = &s->nodes[b];
+        insert_sorted(s, &nb->in_links, &nb->n_in, &nb->cap_in, li, 0);
+    }
+    return ORC_OK;
+}
+
+/* The synthetic traffic of one step: every node, in sorted order, that holds tokens
+ * and has out-links sends ONE token to out-link j with probability thresh / 2^32,
+ * both decided by the counter hash of (seed, step, rank).  Each send is the
+ * reference's SendTokens (node.go:112-131) with n = 1, so it draws one delay. */
+int orc_traffic_sends(orc_sim* s, uint64_t seed, uint32_t thresh, int64_t step) {
+    if (s->status) return s->status;
+    for (int a = 0; a < s->n_nodes; a++) {
+        int v = s->sorted[a];
+        orc_node* n = &s->nodes[v];
+        if (n->tokens <= 0 || n->n_out == 0) continue;
+        uint64_t x = orc_counter_hash(seed, (uint64_t)step, (uint64_t)a);
+        if ((uint32_t)x >= thresh) continue;
+        int j = (int)(((x >> 32) * (uint64_t)n->n_out) >> 32);
+        int rc = send_tokens_idx(s, v, s->links[n->out_links[j]].dest, 1);
+        if (rc) return rc;
+    }
+    return ORC_OK;
+}
+
+/* A synthetic program: for step k in [0, steps): traffic sends (k < traffic_steps),
+ * then the snapshots scheduled at step k in list order (StartSnapshot on rank
+ * snap_rank[i], sim.go:105-123), then Tick (sim.go:71-95).  Nodes are ranks. */
+int orc_run_program(orc_sim* s, int64_t steps, uint64_t traffic_seed, uint32_t thresh,
+                    int64_t traffic_steps, int n_snap, const int32_t* snap_step,
+                    const int32_t* snap_rank) {
+    int si = 0;
+    for (int64_t k = 0; k < steps; k++) {
+        int rc = ORC_OK;
+        if (k < traffic_steps) rc = orc_traffic_sends(s, traffic_seed, thresh, k);
+        while (rc == ORC_OK && si < n_snap && snap_step[si] == k) {
+            rc = start_snapshot_idx(s, s->sorted[snap_rank[si]], NULL);
+            si++;
+        }
+        while (si < n_snap && snap_step[si] < k) si++;
+        if (rc == ORC_OK) rc = orc_tick(s);
+        if (rc) return rc;
+    }
+    return ORC_OK;
+}
+
+/* Snapshot sid by channel: tokens[N] in rank order; channels in (src rank, dest rank)
+ * order; the recorded messages of channel c are vals[off[c] .. off[c+1]) in recording
+ * order.  Works for incomplete snapshots too (what has been recorded so far; nodes
+ * without the local snapshot get tokens -1 and empty channels).  Returns total count
+ * (vals written only below cap). */
+int64_t orc_collect_channels(const orc_sim* s, int sid, int64_t* tokens, int64_t* off, int64_t* vals,
+                             int64_t cap) {
+    int64_t m = 0, c = 0;
+    for (int a = 0; a < s->n_nodes; a++) {
+        const orc_node* n = &s->nodes[s->sorted[a]];
+        const orc_local* l = local_snap((orc_node*)n, sid);
+        tokens[a] = l ? l->num_tokens_in_node : -1;
+    }
+    for (int a = 0; a < s->n_nodes; a++) {
+        const orc_node* src = &s->nodes[s->sorted[a]];
+        for (int k = 0; k < src->n_out; k++, c++) {
+            const orc_link* lk = &s->links[src->out_links[k]];
+            const orc_local* l = local_snap(&s->nodes[lk->dest], sid);
+            off[c] = m;
+            if (!l) continue;
+            const i64vec* v = &l->incoming[in_index(s, lk->dest, lk->src)];
+            for (int64_t q = 0; q < v->n; q++, m++)
+                if (m < cap) vals[m] = v->v[q];
+        }
+    }
+    off[c] = m;
+    return m;
+}
+
+int orc_num_links(const orc_sim* s) { return s->n_links; }
+
+/* Out-channel queue depths in channel order (diagnostics: FIFO sizing). */
+void orc_queue_depths(const orc_sim* s, int64_t* out) {
+    int64_t c = 0;
+    for (int a = 0; a < s->n_nodes; a++) {
+        const orc_node* src = &s->nodes[s->sorted[a]];
+        for (int k = 0; k < src->n_out; k++, c++) out[c] = s->links[src->out_links[k]].q.len;
+    }
 }

@@ -61,6 +61,15 @@ def lib():
             "orc_go_intn_seq": (None, [i64, i32, i64, vp]),
             "orc_run_batch": (C.c_double, [cp, cp, i64, vp, i64, i64, i64, C.c_int,
                                            vp, vp, vp, vp]),
+            "orc_counter_hash": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
+            "orc_counter_delay": (C.c_int, [C.c_uint64, C.c_uint64]),
+            "orc_use_counter_hash": (None, [vp, C.c_uint64]),
+            "orc_build_graph": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, C.c_int]),
+            "orc_traffic_sends": (C.c_int, [vp, C.c_uint64, C.c_uint32, i64]),
+            "orc_run_program": (C.c_int, [vp, i64, C.c_uint64, C.c_uint32, i64, C.c_int, vp, vp]),
+            "orc_collect_channels": (i64, [vp, C.c_int, vp, vp, vp, i64]),
+            "orc_num_links": (C.c_int, [vp]),
+            "orc_queue_depths": (None, [vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -184,6 +193,43 @@ class OracleSim:
     def snapshot_hash(self, sid):
         return self._L.orc_snapshot_hash(self._h, sid)
 
+    # ---- synthetic large-graph workloads ----------------------
+    def use_counter_hash(self, seed):
+        self._L.orc_use_counter_hash(self._h, seed)
+
+    def build_graph(self, tokens, src, dst, width):
+        """Nodes "N%0{width}d" % r with tokens[r]; AddLink(src[i], dst[i]) (ranks)."""
+        tok = np.ascontiguousarray(tokens, dtype=np.int64)
+        s = np.ascontiguousarray(src, dtype=np.int32)
+        d = np.ascontiguousarray(dst, dtype=np.int32)
+        return self._L.orc_build_graph(self._h, tok.size, _ptr(tok), s.size, _ptr(s), _ptr(d), width)
+
+    def run_program(self, steps, traffic_seed, thresh, traffic_steps, snap_step=(), snap_rank=()):
+        ss = np.ascontiguousarray(snap_step, dtype=np.int32)
+        sr = np.ascontiguousarray(snap_rank, dtype=np.int32)
+        return self._L.orc_run_program(self._h, steps, traffic_seed, thresh, traffic_steps, ss.size,
+                                       _ptr(ss), _ptr(sr))
+
+    @property
+    def num_links(self):
+        return self._L.orc_num_links(self._h)
+
+    def queue_depths(self):
+        out = np.zeros(self.num_links, dtype=np.int64)
+        self._L.orc_queue_depths(self._h, _ptr(out))
+        return out
+
+    def collect_channels(self, sid):
+        """(tokens[N] rank order (-1: no local snapshot), offsets[E+1], values) with
+        channels in (src rank, dest rank) order."""
+        n, e = self._L.orc_num_nodes(self._h), self.num_links
+        tok = np.zeros(n, dtype=np.int64)
+        off = np.zeros(e + 1, dtype=np.int64)
+        m = self._L.orc_collect_channels(self._h, sid, _ptr(tok), _ptr(off), None, 0)
+        vals = np.zeros(max(m, 1), dtype=np.int64)
+        self._L.orc_collect_channels(self._h, sid, _ptr(tok), _ptr(off), _ptr(vals), m)
+        return tok, off, vals[:m]
+
     def collect(self, sid):
         n = self._L.orc_num_nodes(self._h)
         tok = np.zeros(n, dtype=np.int64)
@@ -197,6 +243,14 @@ class OracleSim:
         ids = self.node_ids()
         msgs = [(ids[src[i]], ids[dst[i]], int(amt[i])) for i in range(m)]
         return Snapshot(sid, dict(zip(ids, tok.tolist())), msgs)
+
+
+def counter_hash(seed, a, b):
+    return lib().orc_counter_hash(seed, a, b)
+
+
+def counter_delay(seed, k):
+    return lib().orc_counter_delay(seed, k)
 
 
 def run_batch(top_text, events_text, n, sched=None, draws=0, seed_base=REFERENCE_SEED,

@@ -1,0 +1,200 @@
+"""GPU parity of the graph engine (include/clgraph.h) against the reference goldens and
+the CPU oracle.  All comparisons are bit-exact: status, simulator time, final node
+tokens, snapshot completion ticks, token maps, per-channel recorded messages, and the
+reference-level counters (pushes = delay draws, peeks, delivered tokens / markers,
+recorded copies, completed snapshots).
+
+At BASELINE config 4's full size (2^20-node regular digraph, one snapshot under
+continuous traffic) the run is checked through size-independent properties: the
+snapshot completes, its cut is consistent (snapshot tokens + recorded messages =
+total), final tokens + in-flight tokens = total, and reruns are deterministic.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import graphgen as G
+import oracle as O
+from graphcheck import (clg, cl, compare, digest_from_oracle, engine_program, oracle_program,
+                        powerlaw_program, regular_program, scenario_engine, scenario_oracle, Program)
+from snapcheck import assert_equal, check_tokens, read_snapshot_file, scenarios
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("sc", scenarios(), ids=lambda s: s["name"])
+def test_reference_goldens(sc):
+    """The reference's own test_data runs (reference seed) reproduce the golden files."""
+    g = scenario_engine(sc["top"], sc["events"], O.REFERENCE_SEED)
+    assert g.status() == 0
+    actual = []
+    for sid in range(g.num_snapshots):
+        s = g.CollectSnapshot(sid)
+        actual.append((s.id, s.tokenMap, [m.astuple() for m in s.messages]))
+    check_tokens(g.node_tokens(), actual)
+    expected = sorted((read_snapshot_file(f) for f in sc["snaps"]), key=lambda s: s[0])
+    assert len(expected) == len(actual)
+    for e, a in zip(expected, actual):
+        assert_equal(e, a)
+    assert g.time() == sc["ticks"]
+    c = g.counters()
+    assert (c["push"], c["peek"], c["pop_tok"], c["pop_mk"], c["recorded"]) == \
+        (sc["draws"], sc["peek"], sc["pop_tok"], sc["pop_mk"], sc["recorded"])
+
+
+@pytest.mark.parametrize("sc", scenarios(), ids=lambda s: s["name"])
+def test_scenarios_other_seeds_vs_oracle(sc):
+    """Other Go seeds: fatal and hang statuses included, everything bit-exact."""
+    for i in range(1, 17):
+        seed = O.REFERENCE_SEED + 1000 * i
+        compare(scenario_engine(sc["top"], sc["events"], seed), scenario_oracle(sc["top"], sc["events"], seed))
+
+
+@pytest.mark.parametrize("n,steps,seed", [(64, 60, 1), (1000, 80, 2), (4096, 90, 3)])
+def test_regular_traffic_vs_oracle(n, steps, seed):
+    """C4-shaped runs (8-out regular digraph, continuous traffic, snapshots) at sizes the
+    oracle runs in seconds."""
+    p = regular_program(n, steps=steps, seed=seed, snaps=((5, None), (5, 0), (17, None), (30, None)))
+    g = engine_program(p)
+    o = oracle_program(p)
+    assert o.status == 0
+    compare(g, o)
+    sums = g.checksums()
+    assert sums["cut_residual"] == 0 and sums["final_residual"] == 0
+    assert sums["digest"] == digest_from_oracle(o)
+
+
+@pytest.mark.parametrize("n,steps,snaps", [(300, 300, 8), (300, 300, 24), (1500, 400, 48)])
+def test_powerlaw_overlapping_snapshots_vs_oracle(n, steps, snaps):
+    """C5-shaped runs: skewed in-degree hub, one snapshot start per tick, long
+    recording logs, most snapshots still in flight at the end."""
+    p = powerlaw_program(n, steps, snaps, fifo_slots=512)
+    g = engine_program(p)
+    o = oracle_program(p)
+    compare(g, o)
+    assert g.checksums()["digest"] == digest_from_oracle(o)
+
+
+def _random_graph(rng, n):
+    m = int(rng.integers(n, 4 * n))
+    return rng.integers(0, n, m).astype(np.int32), rng.integers(0, n, m).astype(np.int32)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_host_events_vs_oracle(seed):
+    """Random digraphs with host sends of arbitrary sizes (payload history), snapshots
+    at random nodes, ticks, fatals (insufficient tokens, unknown dest) -- string API and
+    Go delay stream, exactly like readEventsFile."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(2, 30))
+    src, dst = _random_graph(rng, n)
+    ids = [f"n{r}" for r in rng.permutation(n)]
+    top = f"{n}\n" + "".join(f"{ids[r]} {int(rng.integers(0, 50))}\n" for r in range(n)) + \
+        "".join(f"{ids[a]} {ids[b]}\n" for a, b in zip(src, dst))
+    ev = []
+    for _ in range(int(rng.integers(5, 40))):
+        x = rng.random()
+        if x < 0.45:
+            a, b = int(rng.integers(0, n)), int(rng.integers(0, n))
+            ev.append(f"send {ids[a]} {ids[b]} {int(rng.integers(0, 8))}")
+        elif x < 0.6:
+            ev.append(f"snapshot {ids[int(rng.integers(0, n))]}")
+        else:
+            ev.append(f"tick {int(rng.integers(1, 4))}")
+    events = "\n".join(ev) + "\n"
+    gseed = O.REFERENCE_SEED + seed
+    g = clg.GraphSim(max_drain_ticks=500)
+    g.read_topology_text(top)
+    g.set_delay_go_seed(gseed)
+    g.read_events_text(events)
+    g.flush()
+    o = O.OracleSim()
+    o.seed_go(gseed)
+    assert o.read_topology_text(top) == 0
+    o.read_events_text(events, 500)
+    compare(g, o)
+
+
+def test_rerun_and_incremental_equal_one_shot():
+    p = regular_program(2000, steps=70, seed=9)
+    g = engine_program(p)
+    first = g.checksums()
+    cnt = g.counters()
+    for _ in range(3):
+        g.rerun()
+        g.synchronize()
+        assert g.checksums() == first
+        assert g.counters() == cnt
+    # the same program flushed tick by tick
+    h = engine_program(p, run=False)
+    inc = clg.GraphSim()
+    inc.set_topology(p.tokens, p.src, p.dst, id_width=p.width())
+    inc.set_delay_hash(p.delay_seed)
+    inc.set_traffic(p.traffic_seed, p.thresh, p.traffic_steps)
+    si = 0
+    for k in range(p.steps):
+        while si < len(p.snap_step) and p.snap_step[si] == k:
+            inc.start_snapshot_rank(int(p.snap_rank[si]))
+            si += 1
+        inc.Tick(1)
+        if k % 7 == 3:
+            inc.flush()
+    inc.flush()
+    assert inc.checksums() == first
+    assert inc.counters() == cnt
+    del h
+
+
+def test_fifo_overflow_status():
+    p = powerlaw_program(300, 200, 24, fifo_slots=2)
+    g = engine_program(p)
+    assert g.status() == cl.INST_FIFO_OVERFLOW
+
+
+def test_explicit_schedule_and_exhaustion():
+    sc = [s for s in scenarios() if s["name"] == "Test8NodesConcurrentSnapshots"][0]
+    from graphcheck import TEST_DATA
+    d = cl.go_delay_schedule(O.REFERENCE_SEED + 5, 1, 200)[0]
+    for length, want in ((200, None), (20, O.DELAY_EXHAUSTED)):
+        g = clg.GraphSim()
+        g.read_topology_file(os.path.join(TEST_DATA, sc["top"]))
+        g.set_delay_schedule(d[:length])
+        g.read_events_file(os.path.join(TEST_DATA, sc["events"]))
+        g.flush()
+        o = O.OracleSim()
+        o.use_schedule(d[:length])
+        o.read_topology(os.path.join(TEST_DATA, sc["top"]))
+        o.read_events(os.path.join(TEST_DATA, sc["events"]))
+        if want is None:
+            compare(g, o)
+        else:   # engine limit: the run freezes at the failing draw
+            assert o.status == want and g.status() == want
+            assert g.time() == o.time
+
+
+def test_c4_full_size_properties():
+    """BASELINE config 4 at full size: 2^20 nodes, 8 random permutations, 100 tokens
+    each, continuous traffic (p = 1/4), one snapshot at step 5."""
+    n, steps = 1 << 20, 80
+    g = clg.GraphSim(fifo_slots=16)
+    g.generate_regular(n, 8, 100, seed=20240)
+    g.set_delay_hash(20241)
+    g.set_traffic(20242, 1 << 30, steps)
+    for k in range(steps):
+        if k == 5:
+            g.start_snapshot_rank(G.mulhi(G.counter_hash(20243, 0, 0), n))
+        g.Tick(1)
+    g.flush()
+    assert g.status() == 0
+    sums = g.checksums()
+    assert sums["completed"] == 1
+    assert sums["cut_residual"] == 0 and sums["final_residual"] == 0
+    c = g.counters()
+    assert c["pop_mk"] == g.num_channels           # one marker per channel
+    assert c["push"] == c["pop_tok"] + c["pop_mk"] + sums["in_flight"]  # unit tokens; no marker left
+    tok, off, msg = g.collect_arrays(0)
+    assert tok.sum() + msg.sum() == 100 * n
+    g.rerun()
+    g.synchronize()
+    assert g.checksums() == sums

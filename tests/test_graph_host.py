@@ -1,0 +1,169 @@
+"""CPU tests of the graph engine's host side (no GPU): the C ABI exports, the counter
+hash against the oracle and the numpy restatement, the synthetic graph generators
+against tests/graphgen.py, topology freezing, argument validation, and that the
+product fails loudly (CL_E_DEVICE) when no gfx950 GPU is present.
+
+The oracle's graph driver is checked here too: its bulk builder must equal the
+reference's own readTopologyFile path, and its runs must conserve tokens and produce
+consistent cuts.
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import graphgen as G
+import oracle as O
+from graphcheck import clg, cl, oracle_program, powerlaw_program, regular_program, digest_from_oracle
+from snapcheck import ROOT, TEST_DATA
+
+HEADER = os.path.join(ROOT, "include", "clgraph.h")
+
+
+def test_exports_every_declared_symbol():
+    names = re.findall(r"^(?:int|uint64_t)\s+(cl_\w+)\(", open(HEADER).read(), re.M)
+    assert len(names) >= 40
+    L = clg.glib()
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_counter_hash_three_ways():
+    rng = np.random.default_rng(5)
+    for _ in range(200):
+        s, a, b = (int(x) for x in rng.integers(0, 2**63, size=3, dtype=np.uint64))
+        want = G.counter_hash(s, a, b)
+        assert clg.counter_hash(s, a, b) == want
+        assert O.counter_hash(s, a, b) == want
+    a = np.arange(1000, dtype=np.uint64)
+    np.testing.assert_array_equal(G.counter_hash_np(7, a, a * 3),
+                                  [G.counter_hash(7, int(x), int(x) * 3) for x in a])
+    for k in range(100):
+        assert O.counter_delay(99, k) == (G.counter_hash(99, k, 0) >> 32) % 5
+
+
+def _edges(g):
+    s, d = g.channels()
+    return s.astype(np.int64), d.astype(np.int64)
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000, 4096])
+def test_regular_generator_matches_restatement(n):
+    g = clg.GraphSim()
+    g.generate_regular(n, 8, 100, seed=1234)
+    s, d = _edges(g)
+    ws, wd = G.regular_graph(n, 8, 1234)
+    np.testing.assert_array_equal(s, ws)
+    np.testing.assert_array_equal(d, wd)
+    assert g.num_nodes == n
+    assert g.node_ids()[0] == "N" + "0" * len(str(n - 1))
+
+
+@pytest.mark.parametrize("n", [3, 100, 2000, 20000])
+def test_powerlaw_generator_matches_restatement(n):
+    g = clg.GraphSim()
+    g.generate_powerlaw(n, 8, 0.9, True, 100, seed=77)
+    s, d = _edges(g)
+    ws, wd = G.powerlaw_graph(n, 8, 0.9, True, 77)
+    np.testing.assert_array_equal(s, ws)
+    np.testing.assert_array_equal(d, wd)
+    indeg = np.bincount(d, minlength=n)
+    if n >= 2000:
+        assert indeg[0] > 20 * np.median(indeg)   # skewed in-degree: rank 0 is the hub
+    assert np.bincount(s, minlength=n).max() <= 10  # bounded out-degree
+
+
+def test_topology_from_top_file_is_rank_ordered():
+    g = clg.GraphSim()
+    g.read_topology_file(os.path.join(TEST_DATA, "10nodes.top"))
+    ids = g.node_ids()
+    assert ids == sorted(ids) and ids[:3] == ["N1", "N10", "N2"]   # getSortedKeys: N10 < N2
+    s, d = g.channels()
+    pairs = list(zip(s.tolist(), d.tolist()))
+    assert pairs == sorted(pairs)
+    o = O.OracleSim()
+    o.read_topology(os.path.join(TEST_DATA, "10nodes.top"))
+    assert o.node_ids() == ids
+
+
+def test_validation_errors():
+    g = clg.GraphSim()
+    g.AddNode("A", 5)
+    with pytest.raises(cl.ClSnapError) as e:
+        g.AddNode("A", 1)
+    assert e.value.code == -3
+    with pytest.raises(cl.ClSnapError) as e:
+        g.AddLink("A", "B")
+    assert e.value.code == -2
+    g.AddNode("B", 0)
+    g.AddLink("A", "B")
+    with pytest.raises(cl.ClSnapError) as e:
+        g.StartSnapshot("C")
+    assert e.value.code == -2
+    g.Tick(1)
+    with pytest.raises(cl.ClSnapError) as e:
+        g.AddNode("C", 1)
+    assert e.value.code == -8
+    with pytest.raises(cl.ClSnapError):
+        g.set_limits(fifo_slots=3)
+    star = clg.GraphSim()
+    with pytest.raises(cl.ClSnapError) as e:   # out-degree above the 64-bit channel mask
+        star.set_topology(np.full(100, 1), np.zeros(99, dtype=np.int32), np.arange(1, 100, dtype=np.int32))
+    assert e.value.code == -7
+
+
+def test_no_gpu_fails_loudly():
+    """The product never falls back to the CPU: without a gfx950 device it raises."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    g = clg.GraphSim()
+    g.read_topology_file(os.path.join(TEST_DATA, "2nodes.top"))
+    g.Tick(1)
+    with pytest.raises(cl.ClSnapError) as e:
+        g.flush()
+    assert e.value.code == -6
+
+
+# ---- the oracle's graph driver ------------------------------------------------------
+
+def test_oracle_bulk_builder_equals_reference_parser():
+    """orc_build_graph + traffic must equal the reference's AddNode/AddLink path."""
+    n = 40
+    src, dst = G.regular_graph(n, 3, 5)
+    text = f"{n}\n" + "".join(f"N{r:02d} {100 + r}\n" for r in range(n)) + \
+        "".join(f"N{a:02d} N{b:02d}\n" for a, b in zip(src, dst))
+    a = O.OracleSim()
+    a.read_topology_text(text)
+    b = O.OracleSim()
+    b.build_graph(100 + np.arange(n), src, dst, 2)
+    for s in (a, b):
+        s.use_counter_hash(3)
+        s.run_program(60, 9, 1 << 30, 60, [4, 9], [3, 17])
+    assert a.counters() == b.counters()
+    assert a.node_tokens() == b.node_tokens()
+    for sid in range(2):
+        ta, oa, va = a.collect_channels(sid)
+        tb, ob, vb = b.collect_channels(sid)
+        np.testing.assert_array_equal(ta, tb)
+        np.testing.assert_array_equal(oa, ob)
+        np.testing.assert_array_equal(va, vb)
+
+
+@pytest.mark.parametrize("kind", ["regular", "powerlaw"])
+def test_oracle_program_conserves_tokens(kind):
+    p = regular_program(512, steps=70) if kind == "regular" else powerlaw_program(300, 300, 8)
+    o = oracle_program(p)
+    assert o.status == 0
+    total = int(p.tokens.sum())
+    done = 0
+    for sid in range(o.num_snapshots):
+        if not o.complete(sid):
+            continue
+        done += 1
+        tok, off, vals = o.collect_channels(sid)
+        assert tok.sum() + vals.sum() == total     # consistent cut
+    assert done >= 1
+    assert o.counters()["draws"] == o.counters()["push"]
+    assert isinstance(digest_from_oracle(o), int)
