@@ -7,6 +7,7 @@
 // (snapshot, node) / (snapshot, channel); each tick is a short sequence of grid-wide
 // phases (pick, marker, expand, tally, scan, push) launched on one HIP stream.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "cl_engine.h"  // mix64, status codes
@@ -33,8 +34,43 @@ constexpr uint32_t kOpen = 0xffffffffu;
 // every later marker adds -1; the operation whose result is exactly kBig completes it.
 constexpr int32_t kBig = 1 << 30;
 constexpr int32_t kGMaxOutDegree = 64;  // non-empty out-channel bitmask per node (u64)
-constexpr int32_t kTallyBlock = 1024;   // nodes per tally/scan block
+constexpr int32_t kGThreads = 256;      // threads (= nodes) per pick / marker / push block
 constexpr int32_t kGStatusHistOverflow = 6;
+// A local snapshot created at a node of in-degree above this is expanded over its
+// in-links by the whole k_push grid instead of by the creating lane.
+constexpr int32_t kSmallIndeg = 64;
+// Counters are kept as per-shard partial sums, cpart[shard * kNumCnt + counter]: every
+// block adds its block-reduced totals to shard blockIdx % kParts, so no address sees
+// more than a few atomics per kernel (a device-scope atomic on one word serializes at
+// ~11 ns, MI355X_MICROARCH.md 'fanin').
+constexpr int32_t kParts = 512;
+enum GCnt : int32_t { GC_PEEK = 0, GC_POP_TOK, GC_POP_MK, GC_PUSH, GC_RECORDED, GC_COMPLETED, kNumCnt = 8 };
+
+// A local snapshot created this tick at a node of in-degree > kSmallIndeg.
+struct BigX {
+  int32_t lo, hi;  // the node's in-CSR range
+  int32_t s0;      // creating sender
+  int32_t sid;
+  int32_t karr;    // in-position of the arriving channel
+  int32_t v;
+  int32_t pad[2];
+};
+
+// A marker delivered this tick (k_pick -> k_marker).
+struct MDel {
+  int32_t s0, v, k, sid;  // sender, receiver, in-position of the channel, snapshot id
+};
+
+// Per in-channel record, by in-CSR position (16 B, one access per delivery / per
+// expanded in-link).
+struct ChIn {
+  uint32_t tokcnt;  // tokens delivered on the channel so far (the recording cursor)
+  uint32_t tick;    // tick of the latest delivery on the channel
+  uint32_t pay;     // payload word of that delivery (kGMarker | sid, or token count)
+  int32_t src;      // sender rank (topology)
+};
+
+constexpr uint32_t kEmpty = 0xffffffffu;  // head receiveTime word of an empty channel
 
 enum GOpKind : int32_t { GOP_SEND = 1, GOP_SNAP = 2 };
 struct GOp {
@@ -45,12 +81,11 @@ struct GOp {
 // Device scalars of one run.
 struct GScal {
   unsigned long long draw;  // next delay draw index (sim.go:101 call count)
-  unsigned long long push, peek, pop_tok, pop_mk, recorded, completed;
   unsigned long long base_trig, base_send;  // this tick's draw bases (scan kernel)
   int32_t status;
-  int32_t mlist_n;  // senders that delivered a marker this tick
-  int32_t xl_n;     // local snapshots created by a marker this tick
+  int32_t big_n;    // creations at high in-degree nodes this tick
   int32_t time;     // simulator time of the last tick that ran (sim.go:13)
+  int32_t pad;
 };
 
 struct GParams {
@@ -65,30 +100,31 @@ struct GParams {
   uint64_t traffic_seed;
   uint32_t traffic_thresh;
   int64_t traffic_steps;
-  int32_t n_blocks;  // tally blocks = ceil(n / kTallyBlock)
+  int32_t n_pblocks;  // node blocks = ceil(n / kGThreads)
+  int32_t pad0;
   // topology (out-CSR channel order = (src rank, dest rank); in-CSR by (dest, src))
   const int32_t* out_off;   // [n+1]
-  const int32_t* ch_dst;    // [e]
-  const int32_t* ch_inpos;  // [e] in-CSR position of channel c
+  const int2* route;        // [e] channel c: (dest rank, in-CSR position)
   const int32_t* in_off;    // [n+1]
-  const int32_t* in_src;    // [e] src rank at in-position k
+  const int32_t* in_src;    // [e] src rank at in-position k (reset source for chin[].src)
   // node state
   int32_t* tokens;     // [n]
-  uint64_t* mask;      // [n] non-empty out-channels (bit = out-index)
   int32_t* pick;       // [n] (tick << 6) | out-index popped in that tick
-  int32_t* trig;       // [n] by sender: out-degree of the node its marker created a snapshot at
-  int32_t* ltrig;      // [n] block-local exclusive prefix of trig
+  int32_t* ltrig;      // [n] block-local exclusive prefix of triggered broadcasts (draws)
   int32_t* lsend;      // [n] block-local exclusive prefix of traffic sends
-  long long* bsum;     // [2 * n_blocks] block sums (trig, send) -> exclusive block offsets
+  long long* bsum;     // [2 * n_pblocks] block sums (trig, send) -> exclusive block offsets
   int32_t* crn;        // [n] snapshots created at the node this tick
   uint64_t* cre;       // [e] by in-CSR range of the node: (s0 << 32) | sid
-  int32_t* mlist;      // [n]
-  int32_t* xl;         // [n]
+  MDel* mlist;         // [n_pblocks * kGThreads] markers delivered, per pick block
+  int32_t* mcnt;       // [n_pblocks]
+  BigX* big;           // [n] creations at nodes of in-degree > kSmallIndeg this tick
+  unsigned long long* cpart;  // [kParts * kNumCnt]
   // channel state
-  uint32_t* hc;        // [e] head (lo16) | count (hi16)
+  // [e] lo32: receiveTime of the head packet (kEmpty if the queue is empty),
+  //     hi32: ring head (lo16) | packets queued (hi16)
+  uint64_t* hq;
   uint64_t* fifo;      // [e << cap_log2]
-  uint32_t* tokcnt;    // [e] by in-position: tokens delivered so far
-  uint64_t* deliv;     // [e] by in-position: (tick << 32) | payload of that tick's delivery
+  ChIn* chin;          // [e] by in-position
   uint32_t* histv;     // [e * hist] by in-position
   // snapshot state
   uint64_t* W;         // [s_cap * n] creation key: (tick << 32) | creating sender (initiator: | 0xffffffff)
@@ -103,7 +139,7 @@ struct GParams {
 
 // Launchers (cg_kernels.hip); return hipError_t as int.
 int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream);
-int cg_launch_tick(const GParams& p, int32_t t, int32_t lanes_per_creation, void* stream);
+int cg_launch_tick(const GParams& p, int32_t t, void* stream);
 int cg_launch_sends(const GParams& p, int32_t t, void* stream);  // step-0 traffic
 int cg_launch_hostops(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream);
 // Recorded copies on channels still recording at the end (out[0] += ...).

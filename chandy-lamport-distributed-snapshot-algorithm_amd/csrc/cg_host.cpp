@@ -150,14 +150,20 @@ struct cl_graph {
   int64_t runs = 0, run_ticks = 0, pending_ticks = 0;
 
   GParams P{};
-  int32_t s_cap = 0, hist = 0, lanes = 1, alloc_cap_log2 = -1;
+  int32_t s_cap = 0, hist = 0, alloc_cap_log2 = -1;
   int64_t sched_len = 0;
-  GBuf<int32_t> d_out_off, d_ch_dst, d_ch_inpos, d_in_off, d_in_src, d_init_tok;
-  GBuf<int32_t> d_tokens, d_pick, d_trig, d_ltrig, d_lsend, d_crn, d_mlist, d_xl;
-  GBuf<uint64_t> d_mask, d_cre;
+  GBuf<int32_t> d_out_off, d_in_off, d_in_src, d_init_tok;
+  GBuf<int2> d_route;
+  GBuf<int32_t> d_tokens, d_pick, d_ltrig, d_lsend, d_crn, d_mcnt;
+  GBuf<MDel> d_mlist;
+  GBuf<ChIn> d_chin;
+  GBuf<BigX> d_big;
+  GBuf<unsigned long long> d_cpart;
+  GBuf<uint64_t> d_cre;
   GBuf<long long> d_bsum;
-  GBuf<uint32_t> d_hc, d_tokcnt, d_histv;
-  GBuf<uint64_t> d_fifo, d_deliv, d_W, d_rec;
+  GBuf<uint32_t> d_histv;
+  GBuf<uint64_t> d_hq;
+  GBuf<uint64_t> d_fifo, d_W, d_rec;
   GBuf<int32_t> d_cnt, d_stok, d_done, d_ctick;
   GBuf<GScal> d_sc;
   GBuf<GOp> d_ops;
@@ -169,13 +175,13 @@ struct cl_graph {
     if (!dev_ready) return;
     (void)hipSetDevice(device);
     (void)hipStreamSynchronize(stream);
-    GBuf<int32_t>* i32s[] = {&d_out_off, &d_ch_dst, &d_ch_inpos, &d_in_off, &d_in_src, &d_init_tok, &d_tokens,
-                             &d_pick,    &d_trig,   &d_ltrig,    &d_lsend,  &d_crn,    &d_mlist,    &d_xl,
-                             &d_cnt,     &d_stok,   &d_done,     &d_ctick};
+    GBuf<int32_t>* i32s[] = {&d_out_off, &d_in_off, &d_in_src, &d_init_tok, &d_tokens,
+                             &d_pick,    &d_ltrig,  &d_lsend,    &d_crn,    &d_mcnt,   &d_cnt,      &d_stok,
+                             &d_done,    &d_ctick};
     for (auto* b : i32s) b->release();
-    d_mask.release(); d_cre.release(); d_bsum.release(); d_hc.release(); d_tokcnt.release(); d_histv.release();
-    d_fifo.release(); d_deliv.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
-    d_sched.release(); d_scratch.release();
+    d_cre.release(); d_bsum.release(); d_hq.release(); d_histv.release(); d_mlist.release(); d_route.release();
+    d_chin.release(); d_fifo.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
+    d_sched.release(); d_scratch.release(); d_big.release(); d_cpart.release();
     for (auto& ev : ev_pool) {
       (void)hipEventDestroy(ev.first);
       (void)hipEventDestroy(ev.second);
@@ -350,8 +356,10 @@ struct cl_graph {
     GHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     dev_ready = true;
     int rc;
-    if ((rc = d_out_off.upload(out_off)) || (rc = d_ch_dst.upload(ch_dst)) || (rc = d_ch_inpos.upload(ch_inpos)) ||
-        (rc = d_in_off.upload(in_off)) || (rc = d_in_src.upload(in_src)) || (rc = d_init_tok.upload(init_tok)))
+    std::vector<int2> route((size_t)e);
+    for (int64_t c = 0; c < e; ++c) route[c] = make_int2(ch_dst[c], ch_inpos[c]);
+    if ((rc = d_out_off.upload(out_off)) || (rc = d_route.upload(route)) || (rc = d_in_off.upload(in_off)) ||
+        (rc = d_in_src.upload(in_src)) || (rc = d_init_tok.upload(init_tok)))
       return rc;
     return CL_OK;
   }
@@ -382,14 +390,16 @@ struct cl_graph {
     hist = std::max(hist, want_h);
     alloc_cap_log2 = cap_log2;
     const size_t N = (size_t)n, E = (size_t)std::max<int64_t>(e, 1);
+    const size_t NP = (N + kGThreads - 1) / kGThreads;
     if ((uint64_t)s_cap * N >= (1ull << 40) || (uint64_t)s_cap * E >= (1ull << 40))
       return gerr(CL_E_LIMIT, "snapshot state too large");
     int rc;
-    if ((rc = d_tokens.ensure(N)) || (rc = d_pick.ensure(N)) || (rc = d_trig.ensure(N)) || (rc = d_ltrig.ensure(N)) ||
-        (rc = d_lsend.ensure(N)) || (rc = d_crn.ensure(N)) || (rc = d_mlist.ensure(N)) || (rc = d_xl.ensure(N)) ||
-        (rc = d_mask.ensure(N)) || (rc = d_cre.ensure(E)) || (rc = d_bsum.ensure(2 * ((N + kTallyBlock - 1) / kTallyBlock))) ||
-        (rc = d_hc.ensure(E)) || (rc = d_tokcnt.ensure(E)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
-        (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_deliv.ensure(E)) || (rc = d_W.ensure(s_cap * N)) ||
+    if ((rc = d_tokens.ensure(N)) || (rc = d_pick.ensure(N)) || (rc = d_ltrig.ensure(N)) ||
+        (rc = d_lsend.ensure(N)) || (rc = d_crn.ensure(N)) || (rc = d_mlist.ensure(NP * kGThreads)) ||
+        (rc = d_mcnt.ensure(NP)) || (rc = d_big.ensure(N)) || (rc = d_cpart.ensure((size_t)kParts * kNumCnt)) ||
+        (rc = d_cre.ensure(E)) || (rc = d_bsum.ensure(2 * NP)) || (rc = d_hq.ensure(E)) ||
+        (rc = d_chin.ensure(E)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
+        (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_W.ensure(s_cap * N)) ||
         (rc = d_rec.ensure(s_cap * E)) || (rc = d_cnt.ensure(s_cap * N)) || (rc = d_stok.ensure(s_cap * N)) ||
         (rc = d_done.ensure(s_cap)) || (rc = d_ctick.ensure(s_cap)) || (rc = d_sc.ensure(1)) ||
         (rc = d_scratch.ensure(3 + (size_t)s_cap)))
@@ -431,27 +441,25 @@ struct cl_graph {
     p.traffic_seed = traffic_seed;
     p.traffic_thresh = traffic_thresh;
     p.traffic_steps = traffic_steps;
-    p.n_blocks = (n + kTallyBlock - 1) / kTallyBlock;
+    p.n_pblocks = (n + kGThreads - 1) / kGThreads;
     p.out_off = d_out_off.p;
-    p.ch_dst = d_ch_dst.p;
-    p.ch_inpos = d_ch_inpos.p;
+    p.route = d_route.p;
     p.in_off = d_in_off.p;
     p.in_src = d_in_src.p;
     p.tokens = d_tokens.p;
-    p.mask = d_mask.p;
     p.pick = d_pick.p;
-    p.trig = d_trig.p;
     p.ltrig = d_ltrig.p;
     p.lsend = d_lsend.p;
     p.bsum = d_bsum.p;
     p.crn = d_crn.p;
     p.cre = d_cre.p;
     p.mlist = d_mlist.p;
-    p.xl = d_xl.p;
-    p.hc = d_hc.p;
+    p.mcnt = d_mcnt.p;
+    p.big = d_big.p;
+    p.cpart = d_cpart.p;
+    p.hq = d_hq.p;
     p.fifo = d_fifo.p;
-    p.tokcnt = d_tokcnt.p;
-    p.deliv = d_deliv.p;
+    p.chin = d_chin.p;
     p.histv = d_histv.p;
     p.W = d_W.p;
     p.cnt = d_cnt.p;
@@ -461,10 +469,6 @@ struct cl_graph {
     p.ctick = d_ctick.p;
     p.sc = d_sc.p;
     p.ops = d_ops.p;
-    // lanes per created local snapshot in k_expand: about the mean in-degree
-    const int64_t mean = e > 0 ? (e + n - 1) / n : 1;
-    lanes = 1;
-    while (lanes < mean && lanes < 64) lanes <<= 1;
   }
 
   int upload_ops() {
@@ -485,7 +489,7 @@ struct cl_graph {
     if (time + 1 > kMaxGraphTime) return gerr(CL_E_LIMIT, "simulated time would exceed %lld ticks", (long long)kMaxGraphTime);
     ++time;
     ++run_ticks;
-    return k_err(cg_launch_tick(P, (int32_t)time, lanes, stream));
+    return k_err(cg_launch_tick(P, (int32_t)time, stream));
   }
 
   int flush_hostops(size_t& pend_begin, size_t& pend_count) {
@@ -586,6 +590,18 @@ struct cl_graph {
     executed = prog.size();
     state_valid = true;
     ++runs;
+    return CL_OK;
+  }
+
+  // Counter totals: sum of the per-shard partials (cg_engine.h kParts).
+  int counter_totals(uint64_t* out) {
+    std::vector<unsigned long long> part((size_t)kParts * kNumCnt);
+    GHIP(hipMemcpyAsync(part.data(), d_cpart.p, part.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                        stream));
+    GHIP(hipStreamSynchronize(stream));
+    for (int c = 0; c < kNumCnt; ++c) out[c] = 0;
+    for (int sh = 0; sh < kParts; ++sh)
+      for (int c = 0; c < kNumCnt; ++c) out[c] += part[(size_t)sh * kNumCnt + c];
     return CL_OK;
   }
 
@@ -987,11 +1003,12 @@ int cl_graph_device_bytes(cl_graph* g, int64_t* bytes) {
   G_CHECK(g);
   if (!bytes) return gerr(CL_E_INVALID, "null output");
   size_t b = 0;
-  b += g->d_out_off.bytes() + g->d_ch_dst.bytes() + g->d_ch_inpos.bytes() + g->d_in_off.bytes() +
-       g->d_in_src.bytes() + g->d_init_tok.bytes() + g->d_tokens.bytes() + g->d_pick.bytes() + g->d_trig.bytes() +
-       g->d_ltrig.bytes() + g->d_lsend.bytes() + g->d_crn.bytes() + g->d_mlist.bytes() + g->d_xl.bytes() +
-       g->d_mask.bytes() + g->d_cre.bytes() + g->d_bsum.bytes() + g->d_hc.bytes() + g->d_tokcnt.bytes() +
-       g->d_histv.bytes() + g->d_fifo.bytes() + g->d_deliv.bytes() + g->d_W.bytes() + g->d_rec.bytes() +
+  b += g->d_out_off.bytes() + g->d_route.bytes() + g->d_in_off.bytes() +
+       g->d_in_src.bytes() + g->d_init_tok.bytes() + g->d_tokens.bytes() + g->d_pick.bytes() + g->d_chin.bytes() +
+       g->d_ltrig.bytes() + g->d_lsend.bytes() + g->d_crn.bytes() + g->d_mlist.bytes() + g->d_mcnt.bytes() +
+       g->d_big.bytes() + g->d_cpart.bytes() +
+       g->d_cre.bytes() + g->d_bsum.bytes() + g->d_hq.bytes() +
+       g->d_histv.bytes() + g->d_fifo.bytes() + g->d_W.bytes() + g->d_rec.bytes() +
        g->d_cnt.bytes() + g->d_stok.bytes() + g->d_done.bytes() + g->d_ctick.bytes() + g->d_sched.bytes();
   *bytes = (int64_t)b;
   return CL_OK;
@@ -1095,15 +1112,17 @@ int cl_graph_get_counters(cl_graph* g, int64_t* out) {
   if ((rc = g->k_err(cg_launch_finish(g->P, g->n_sids, g->d_scratch.p, g->stream)))) return rc;
   GScal sc;
   unsigned long long open = 0;
+  uint64_t cnt[kNumCnt];
+  if ((rc = g->counter_totals(cnt))) return rc;
   GHIP(hipMemcpyAsync(&sc, g->d_sc.p, sizeof sc, hipMemcpyDeviceToHost, g->stream));
   GHIP(hipMemcpyAsync(&open, g->d_scratch.p, sizeof open, hipMemcpyDeviceToHost, g->stream));
   GHIP(hipStreamSynchronize(g->stream));
-  out[CL_CNT_PUSH] = (int64_t)sc.push;
-  out[CL_CNT_PEEK] = (int64_t)sc.peek;
-  out[CL_CNT_POP_TOKEN] = (int64_t)sc.pop_tok;
-  out[CL_CNT_POP_MARKER] = (int64_t)sc.pop_mk;
-  out[CL_CNT_RECORDED] = (int64_t)(sc.recorded + open);
-  out[CL_CNT_COMPLETED] = (int64_t)sc.completed;
+  out[CL_CNT_PUSH] = (int64_t)cnt[GC_PUSH];
+  out[CL_CNT_PEEK] = (int64_t)cnt[GC_PEEK];
+  out[CL_CNT_POP_TOKEN] = (int64_t)cnt[GC_POP_TOK];
+  out[CL_CNT_POP_MARKER] = (int64_t)cnt[GC_POP_MK];
+  out[CL_CNT_RECORDED] = (int64_t)(cnt[GC_RECORDED] + open);
+  out[CL_CNT_COMPLETED] = (int64_t)cnt[GC_COMPLETED];
   out[CL_CNT_INSTANCES] = 1;
   out[CL_CNT_TICKS] = sc.status ? sc.time : g->time;
   return CL_OK;
@@ -1134,7 +1153,9 @@ int cl_graph_get_checksums(cl_graph* g, int64_t* out) {
   }
   const int64_t fin = (int64_t)r[0] + (int64_t)r[1] - g->total_tokens;
   out[CL_GSUM_OK] = (sc.status == 0 && !g->hang) ? 1 : 0;
-  out[CL_GSUM_DELIVERED] = (int64_t)(sc.pop_tok + sc.pop_mk);
+  uint64_t cnt[kNumCnt];
+  if ((rc = g->counter_totals(cnt))) return rc;
+  out[CL_GSUM_DELIVERED] = (int64_t)(cnt[GC_POP_TOK] + cnt[GC_POP_MK]);
   out[CL_GSUM_COMPLETED] = completed;
   out[CL_GSUM_CUT_RESIDUAL] = cut;
   out[CL_GSUM_FINAL_RESIDUAL] = fin < 0 ? -fin : fin;

@@ -1,31 +1,34 @@
 // cg_kernels.hip -- gfx950 kernels of the graph engine: one reference simulation over a
-// large topology, state in HBM, one tick = a short sequence of grid-wide phases.
+// large topology, state in HBM, one tick = four grid-wide phases on one HIP stream.
 //
 // Reference semantics restated per phase (paths relative to /root/reference/chandy_lamport):
 //   k_pick     Tick (sim.go:71-95): time++, every sender scans its out-links in dest
 //              order and pops the first due head (at most one per sender, :90).  Picks
 //              from tick-start state equal the reference's sequential picks: a push made
 //              during tick t is due at >= t+1 and never changes a non-empty queue's head.
-//              Tokens are applied at once (HandleToken node.go:174-185 is commutative for
-//              the token count; recording is the channel cursor tokcnt); markers are
-//              staged for k_marker.
+//              The scan reads only the per-channel head receiveTime words (contiguous per
+//              sender); the FIFO itself is touched only by the pop.  Tokens are applied at
+//              once (HandleToken node.go:174-185 is commutative for the token count;
+//              recording is the channel cursor tokcnt); markers are staged for k_marker.
 //   k_marker   HandleMarker (node.go:149-171): the first marker of snapshot s at node v
 //              is the one from the lowest-ranked sender in the earliest tick (atomicMin on
 //              the creation key W); it creates the local snapshot (CreateLocalSnapshot
 //              node.go:58-84) and triggers the broadcast; later markers close their
 //              channel.  Completion (node.go:165-168, sim.go:126-131) is the pending
-//              accumulator reaching exactly kBig.
-//   k_expand   The per-in-link part of CreateLocalSnapshot: recording cursors begin at
-//              the channel's delivered-token count AT the creating delivery, i.e. tokens
+//              accumulator reaching exactly kBig.  The creating lane also expands the
+//              local snapshot over the node's in-links: recording cursors begin at the
+//              channel's delivered-token count AT the creating delivery, i.e. tokens
 //              delivered in the same tick by lower-ranked senders are before it and those
 //              of higher-ranked senders after it; the recorded node tokens likewise.
-//   k_tally    } SendToNeighbors (node.go:97-109) draws one delay per out-link in the
-//   k_scan     } reference's global draw order: triggering senders in rank order, then
-//   k_push     } the next step's sends in rank order; a two-level exclusive scan over
-//              node ranks gives every broadcast/send its draw index.  Each node then
-//              pushes onto its own out-channels (broadcasts in creating-sender order,
-//              then its send), so FIFO order is the reference's Queue.Push order
-//              (queue.go:18-20).
+//              Each block also tallies, for its 256 node ranks, the broadcasts its
+//              senders triggered and the next step's traffic sends.
+//   k_scan     SendToNeighbors (node.go:97-109) draws one delay per out-link in the
+//              reference's global draw order -- triggering senders in rank order, then
+//              the next step's sends in rank order: exclusive scan of the block tallies.
+//   k_push     Every node pushes onto its own out-channels: the broadcasts of the local
+//              snapshots created at it this tick (in creating-sender order), then its
+//              send, so FIFO order is the reference's Queue.Push order (queue.go:18-20).
+//              The grid then expands local snapshots created at high in-degree nodes.
 //   k_hostops  ProcessEvent for host events (sim.go:58-68, SendTokens node.go:112-131,
 //              StartSnapshot sim.go:105-123 / node.go:198-212), in program order.
 #include <hip/hip_runtime.h>
@@ -35,34 +38,46 @@
 namespace clsnap {
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = kGThreads;
 
 __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
-
-__device__ inline uint32_t lanes_below(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// Wave-aggregated append: one atomic per wave, slots in lane order.
-__device__ inline int wave_append(int32_t* counter, bool pred) {
-  const uint64_t m = __ballot(pred);
-  if (m == 0) return -1;
-  const int leader = __ffsll((unsigned long long)m) - 1;
-  int base = 0;
-  if ((int)lane_id() == leader) base = atomicAdd(counter, (int)__popcll(m));
-  base = __shfl(base, leader);
-  return pred ? base + (int)lanes_below(m) : -1;
-}
 
 __device__ inline unsigned long long wave_sum(unsigned long long x) {
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
   return x;
 }
 
-// Add a per-lane count to a device counter, one atomic per wave.
+// Add a per-lane count to a device counter, one atomic per wave (result kernels only).
 __device__ inline void wave_count(unsigned long long* dst, unsigned long long x) {
   x = wave_sum(x);
   if (lane_id() == 0 && x) atomicAdd(dst, x);
+}
+
+// Block-reduce NV per-thread counts and add them to this block's counter shard.  Every
+// thread of the block must call it (it has a barrier).
+template <int NV>
+__device__ inline void block_count(const GParams& p, const int (&idx)[NV], unsigned long long (&x)[NV]) {
+  __shared__ unsigned long long sh[NV][kGThreads / 64];
+  const int w = threadIdx.x >> 6;
+  for (int i = 0; i < NV; ++i) {
+    x[i] = wave_sum(x[i]);
+    if (lane_id() == 0) sh[i][w] = x[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    unsigned long long t = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += sh[threadIdx.x][k];
+    if (t) atomicAdd(&p.cpart[(blockIdx.x & (kParts - 1)) * kNumCnt + idx[threadIdx.x]], t);
+  }
+}
+
+// Frozen-run check, uniform over the block (a status set by another block of the same
+// kernel must not split a block at a barrier).
+__device__ inline bool block_frozen(const GParams& p) {
+  __shared__ int s_frozen;
+  if (threadIdx.x == 0) s_frozen = p.sc->status;
+  __syncthreads();
+  return s_frozen != 0;
 }
 
 __device__ inline void set_status(GScal* sc, int32_t code) { atomicCAS(&sc->status, 0, code); }
@@ -81,18 +96,18 @@ __device__ inline uint32_t receive_time(const GParams& p, uint64_t k, int32_t ti
   return (uint32_t)time + 1u + d;
 }
 
-// Queue.Push (queue.go:18-20) onto out-channel j of node v.
-__device__ inline void push_entry(const GParams& p, int32_t c, int32_t j, uint64_t& mask, uint32_t payload,
-                                  uint32_t rt, unsigned long long& pushes) {
-  const uint32_t hc = p.hc[c];
+// Queue.Push (queue.go:18-20) onto channel c.
+__device__ inline void push_entry(const GParams& p, int32_t c, uint32_t payload, uint32_t rt,
+                                  unsigned long long& pushes) {
+  const uint64_t q = p.hq[c];
+  const uint32_t hc = (uint32_t)(q >> 32);
   const uint32_t head = hc & 0xffffu, cnt = hc >> 16, cap = 1u << p.cap_log2;
   if (cnt >= cap) {
     set_status(p.sc, ST_FIFO_OVERFLOW);
     return;
   }
   p.fifo[((size_t)c << p.cap_log2) + ((head + cnt) & (cap - 1))] = ((uint64_t)rt << 32) | payload;
-  p.hc[c] = head | ((cnt + 1) << 16);
-  mask |= 1ull << j;
+  p.hq[c] = ((uint64_t)(head | ((cnt + 1) << 16)) << 32) | (cnt == 0 ? rt : (uint32_t)q);
   ++pushes;
 }
 
@@ -106,179 +121,23 @@ __device__ inline bool traffic_send(const GParams& p, int64_t step, int32_t v, i
   return true;
 }
 
-__device__ inline void complete_node(const GParams& p, int32_t sid, int32_t t, unsigned long long& completed) {
-  const int d = atomicAdd(&p.done[sid], 1) + 1;  // NotifyCompletedSnapshot, sim.go:126-131
-  if (d == p.n) {
-    p.ctick[sid] = t;
-    ++completed;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// reset
-// ---------------------------------------------------------------------------
-__global__ void k_reset_nodes(GParams p, const int32_t* init_tok) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v < p.n) {
-    p.tokens[v] = init_tok[v];
-    p.mask[v] = 0;
-    p.pick[v] = -1;
-    p.trig[v] = 0;
-    p.crn[v] = 0;
-  }
-  if (v < p.s_cap) {
-    p.done[v] = 0;
-    p.ctick[v] = -1;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// tick phase A: pick + deliver
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_pick(GParams p, int32_t t) {
-  if (p.sc->status) return;
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s == 0) p.sc->time = t;  // time++ (sim.go:72)
-  unsigned long long peeks = 0, ptok = 0, pmk = 0;
-  bool marker = false;
-  if (s < p.n) {
-    uint64_t m = p.mask[s];
-    if (m) {
-      const uint64_t m0 = m;
-      const int32_t base = p.out_off[s];
-      const uint32_t capm = (1u << p.cap_log2) - 1;
-      while (m) {
-        const int j = __builtin_ctzll(m);
-        m &= m - 1;
-        const int32_t c = base + j;
-        const uint32_t hc = p.hc[c];
-        const uint32_t head = hc & 0xffffu;
-        const uint64_t e = p.fifo[((size_t)c << p.cap_log2) + head];
-        ++peeks;  // Queue.Peek, sim.go:83
-        if ((uint32_t)(e >> 32) > (uint32_t)t) continue;
-        const uint32_t cnt = (hc >> 16) - 1;
-        p.hc[c] = ((head + 1) & capm) | (cnt << 16);
-        if (cnt == 0) p.mask[s] = m0 & ~(1ull << j);
-        p.pick[s] = (t << 6) | j;
-        const int32_t v = p.ch_dst[c], k = p.ch_inpos[c];
-        const uint32_t pay = (uint32_t)e;
-        if (pay & kGMarker) {
-          const uint32_t sid = pay & kGPayload;
-          atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + v], ((unsigned long long)t << 32) | (uint32_t)s);
-          marker = true;
-          ++pmk;
-        } else {
-          atomicAdd(&p.tokens[v], (int32_t)pay);  // HandleToken node.go:175
-          const uint32_t tc = p.tokcnt[k];
-          if (p.hist) {
-            if (tc < (uint32_t)p.hist) p.histv[(size_t)k * p.hist + tc] = pay;
-            else set_status(p.sc, kGStatusHistOverflow);
-          }
-          p.tokcnt[k] = tc + 1;
-          ++ptok;
-        }
-        p.deliv[k] = ((uint64_t)t << 32) | pay;
-        break;
+// NotifyCompletedSnapshot (sim.go:126-131) for every lane with `done`: one atomic per
+// distinct snapshot id in the wave; the add that reaches N completes the snapshot.
+__device__ inline void complete_nodes(const GParams& p, bool done, int32_t sid, int32_t t,
+                                      unsigned long long& completed) {
+  uint64_t m = __ballot(done);
+  while (m) {
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    const int32_t lsid = __shfl(sid, leader);
+    const uint64_t same = __ballot(done && sid == lsid);
+    if ((int)lane_id() == leader) {
+      const int c = (int)__popcll(same);
+      if (atomicAdd(&p.done[lsid], c) + c == p.n) {
+        p.ctick[lsid] = t;
+        ++completed;
       }
     }
-  }
-  const int slot = wave_append(&p.sc->mlist_n, marker);
-  if (marker) p.mlist[slot] = s;
-  wave_count(&p.sc->peek, peeks);
-  wave_count(&p.sc->pop_tok, ptok);
-  wave_count(&p.sc->pop_mk, pmk);
-}
-
-// ---------------------------------------------------------------------------
-// tick phase B: markers
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_marker(GParams p, int32_t t) {
-  if (p.sc->status) return;
-  const int nm = p.sc->mlist_n;
-  unsigned long long recorded = 0, completed = 0;
-  const int stride = gridDim.x * blockDim.x;
-  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
-  // uniform trip count per wave so wave_append sees every lane
-  const int trips = (nm + stride - 1) / stride;
-  for (int it = 0; it < trips; ++it) {
-    const int i = i0 + it * stride;
-    bool creator = false;
-    int32_t s0 = 0;
-    if (i < nm) {
-      s0 = p.mlist[i];
-      const int32_t c = p.out_off[s0] + (p.pick[s0] & 63);
-      const int32_t v = p.ch_dst[c], k = p.ch_inpos[c];
-      const int32_t sid = (int32_t)((uint32_t)p.deliv[k] & kGPayload);
-      const size_t sv = (size_t)sid * p.n + v;
-      const uint64_t key = p.W[sv];
-      const int32_t indeg = p.in_off[v + 1] - p.in_off[v];
-      if (key == (((uint64_t)t << 32) | (uint32_t)s0)) {
-        // first marker: CreateLocalSnapshot(src) + SendToNeighbors (node.go:153-156)
-        creator = true;
-        p.trig[s0] = p.out_off[v + 1] - p.out_off[v];
-        const int slot = atomicAdd(&p.crn[v], 1);
-        p.cre[p.in_off[v] + slot] = ((uint64_t)(uint32_t)s0 << 32) | (uint32_t)sid;
-        const int add = kBig + indeg - 1;
-        if (atomicAdd(&p.cnt[sv], add) + add == kBig) complete_node(p, sid, t, completed);
-      } else {
-        // later marker: stop recording the channel (node.go:158-160)
-        if ((key >> 32) != (uint64_t)t) {  // created in an earlier tick: cursors exist
-          const uint32_t e = p.tokcnt[k];
-          uint32_t* r = (uint32_t*)&p.rec[(size_t)sid * p.e + k];
-          recorded += e - r[0];
-          r[1] = e;
-        }  // else created this tick by a lower-ranked sender: k_expand closes it
-        if (atomicAdd(&p.cnt[sv], -1) - 1 == kBig) complete_node(p, sid, t, completed);
-      }
-    }
-    const int slot = wave_append(&p.sc->xl_n, creator);
-    if (creator) p.xl[slot] = s0;
-  }
-  wave_count(&p.sc->recorded, recorded);
-  wave_count(&p.sc->completed, completed);
-}
-
-// ---------------------------------------------------------------------------
-// tick phase C: expand the local snapshots created this tick over their in-links.
-// `L` lanes cooperate on one creation (L = power of two <= 64).
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_expand(GParams p, int32_t t, int32_t L) {
-  if (p.sc->status) return;
-  const int nx = p.sc->xl_n;
-  const int gtid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = gtid & (L - 1);
-  const int groups = gridDim.x * blockDim.x / L;
-  const int trips = (nx + groups - 1) / groups;
-  for (int it = 0; it < trips; ++it) {
-    const int i = gtid / L + it * groups;
-    int tsum = 0;
-    int32_t v = 0, sid = 0;
-    if (i < nx) {
-      const int32_t s0 = p.xl[i];
-      const int32_t c = p.out_off[s0] + (p.pick[s0] & 63);
-      v = p.ch_dst[c];
-      const int32_t karr = p.ch_inpos[c];
-      sid = (int32_t)((uint32_t)p.deliv[karr] & kGPayload);
-      const int32_t lo = p.in_off[v], hi = p.in_off[v + 1];
-      uint64_t* rec = p.rec + (size_t)sid * p.e;
-      for (int32_t k = lo + lane; k < hi; k += L) {
-        uint32_t b = p.tokcnt[k];
-        const uint64_t dv = p.deliv[k];
-        bool closed = k == karr;  // the arriving channel does not record (node.go:66-69)
-        if ((dv >> 32) == (uint64_t)t && p.in_src[k] > s0) {
-          const uint32_t pay = (uint32_t)dv;
-          if (!(pay & kGMarker)) {
-            b -= 1;  // delivered after the creating marker: recorded
-            tsum += (int)pay;
-          } else if ((int32_t)(pay & kGPayload) == sid) {
-            closed = true;  // its own marker arrives later in the same tick
-          }
-        }
-        rec[k] = (uint64_t)b | ((uint64_t)(closed ? b : kOpen) << 32);
-      }
-    }
-    for (int o = L >> 1; o > 0; o >>= 1) tsum += __shfl_xor(tsum, o, L);
-    if (i < nx && lane == 0) p.stok[(size_t)sid * p.n + v] = p.tokens[v] - tsum;
+    m &= ~same;
   }
 }
 
@@ -316,55 +175,217 @@ __device__ inline void block_exclusive_scan2(long long& a, long long& b, long lo
   b = pb + ib - b;
 }
 
-// ---------------------------------------------------------------------------
-// tick phase D: tally triggers (this tick) and traffic sends (step `step`) per block
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_tally(GParams p, int32_t step) {
-  if (p.sc->status) return;
-  __shared__ long long sh[32];
-  const int base = blockIdx.x * kTallyBlock + threadIdx.x * 4;
-  int tr[4], se[4];
-  long long a = 0, b = 0;
-  for (int q = 0; q < 4; ++q) {
-    const int v = base + q;
-    tr[q] = se[q] = 0;
-    if (v < p.n) {
-      tr[q] = p.trig[v];
-      if (tr[q]) p.trig[v] = 0;
-      int32_t j;
-      se[q] = traffic_send(p, step, v, p.out_off[v + 1] - p.out_off[v], p.tokens[v], &j) ? 1 : 0;
-    }
-    a += tr[q];
-    b += se[q];
+// Block tally of node rank v = blockIdx.x * kGThreads + threadIdx.x: `trig` draws
+// triggered by v's delivery this tick, and v's traffic send of step `step`.
+__device__ inline void tally(const GParams& p, int32_t trig, int32_t step) {
+  __shared__ long long sh[2 * (kGThreads / 64)];
+  const int v = blockIdx.x * kGThreads + threadIdx.x;
+  long long a = trig, b = 0;
+  if (v < p.n) {
+    int32_t j;
+    b = traffic_send(p, step, v, p.out_off[v + 1] - p.out_off[v], p.tokens[v], &j) ? 1 : 0;
   }
+  const long long a0 = a, b0 = b;
   long long ta, tb;
   block_exclusive_scan2(a, b, ta, tb, sh);
-  for (int q = 0; q < 4; ++q) {
-    const int v = base + q;
-    if (tr[q]) p.ltrig[v] = (int32_t)a;
-    if (se[q]) p.lsend[v] = (int32_t)b;
-    a += tr[q];
-    b += se[q];
-  }
+  if (a0) p.ltrig[v] = (int32_t)a;
+  if (b0) p.lsend[v] = (int32_t)b;
   if (threadIdx.x == 0) {
     p.bsum[2 * blockIdx.x] = ta;
     p.bsum[2 * blockIdx.x + 1] = tb;
   }
 }
 
-// phase E: exclusive scan of the block sums (one workgroup), draw bases
+// Expand a local snapshot created at v by s0's marker over in-links [lo, hi) (stride
+// `step`): cursor pairs, and the token payloads delivered after the creating marker.
+__device__ inline int expand_range(const GParams& p, int32_t t, int32_t s0, int32_t sid, int32_t karr,
+                                   int32_t lo, int32_t hi, int32_t step) {
+  int tsum = 0;
+  uint64_t* rec = p.rec + (size_t)sid * p.e;
+  for (int32_t k = lo; k < hi; k += step) {
+    const ChIn ci = p.chin[k];
+    uint32_t b = ci.tokcnt;
+    bool closed = k == karr;  // the arriving channel does not record (node.go:66-69)
+    if (ci.tick == (uint32_t)t && ci.src > s0) {
+      if (!(ci.pay & kGMarker)) {
+        b -= 1;  // delivered after the creating marker: recorded
+        tsum += (int)ci.pay;
+      } else if ((int32_t)(ci.pay & kGPayload) == sid) {
+        closed = true;  // its own marker arrives later in the same tick
+      }
+    }
+    rec[k] = (uint64_t)b | ((uint64_t)(closed ? b : kOpen) << 32);
+  }
+  return tsum;
+}
+
+// ---------------------------------------------------------------------------
+// reset
+// ---------------------------------------------------------------------------
+__global__ void k_reset(GParams p, const int32_t* init_tok) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < (size_t)p.n) {
+    p.tokens[i] = init_tok[i];
+    p.pick[i] = -1;
+    p.crn[i] = 0;
+  }
+  if (i < (size_t)p.e) {
+    p.chin[i] = ChIn{0u, 0u, 0u, p.in_src[i]};
+    p.hq[i] = kEmpty;
+  }
+  if (i < (size_t)p.s_cap) {
+    p.done[i] = 0;
+    p.ctick[i] = -1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// tick phase A: pick + deliver
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
+  if (block_frozen(p)) return;
+  __shared__ int s_m;
+  if (threadIdx.x == 0) s_m = 0;
+  __syncthreads();
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s == 0) {
+    p.sc->time = t;  // time++ (sim.go:72)
+    p.sc->big_n = 0;
+  }
+  unsigned long long c[3] = {0, 0, 0};  // peek, pop_tok, pop_mk
+  if (s < p.n) {
+    const int32_t base = p.out_off[s], od = p.out_off[s + 1] - base;
+    for (int j = 0; j < od; ++j) {
+      const uint64_t q = p.hq[base + j];
+      const uint32_t rt = (uint32_t)q;
+      if (rt == kEmpty) continue;
+      ++c[0];  // Queue.Peek, sim.go:83
+      if (rt > (uint32_t)t) continue;
+      const int32_t ch = base + j;
+      const uint32_t hc = (uint32_t)(q >> 32), capm = (1u << p.cap_log2) - 1;
+      const uint32_t head = hc & 0xffffu, cnt = (hc >> 16) - 1;
+      const size_t ring = (size_t)ch << p.cap_log2;
+      const int2 rte = p.route[ch];
+      const uint32_t pay = (uint32_t)p.fifo[ring + head];
+      const uint32_t nrt = cnt ? (uint32_t)(p.fifo[ring + ((head + 1) & capm)] >> 32) : kEmpty;
+      p.hq[ch] = ((uint64_t)(((head + 1) & capm) | (cnt << 16)) << 32) | nrt;
+      p.pick[s] = (t << 6) | j;
+      const int32_t v = rte.x, k = rte.y;
+      ChIn* ci = &p.chin[k];
+      ci->tick = (uint32_t)t;
+      ci->pay = pay;
+      if (pay & kGMarker) {
+        const int32_t sid = (int32_t)(pay & kGPayload);
+        atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + v], ((unsigned long long)t << 32) | (uint32_t)s);
+        p.mlist[blockIdx.x * kGThreads + atomicAdd(&s_m, 1)] = MDel{s, v, k, sid};
+        ++c[2];
+      } else {
+        atomicAdd(&p.tokens[v], (int32_t)pay);  // HandleToken node.go:175
+        const uint32_t tc = ci->tokcnt;
+        if (p.hist) {
+          if (tc < (uint32_t)p.hist) p.histv[(size_t)k * p.hist + tc] = pay;
+          else set_status(p.sc, kGStatusHistOverflow);
+        }
+        ci->tokcnt = tc + 1;
+        ++c[1];
+      }
+      break;
+    }
+  }
+  const int idx[3] = {GC_PEEK, GC_POP_TOK, GC_POP_MK};
+  block_count<3>(p, idx, c);
+  if (threadIdx.x == 0) p.mcnt[blockIdx.x] = s_m;
+}
+
+// ---------------------------------------------------------------------------
+// tick phase B: the markers delivered by pick block b's senders, and block b's tally
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t t) {
+  if (block_frozen(p)) return;
+  __shared__ int s_nb, s_base;
+  __shared__ int s_trig[kGThreads];
+  s_trig[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_nb = 0;
+  __syncthreads();
+  const int nm = p.mcnt[blockIdx.x];
+  unsigned long long c[2] = {0, 0};  // recorded, completed
+  bool done = false;
+  int32_t sid = 0;
+  int bslot = -1;
+  BigX bx;
+  if ((int)threadIdx.x < nm) {
+    const MDel m = p.mlist[blockIdx.x * kGThreads + threadIdx.x];
+    const int32_t s0 = m.s0, v = m.v, k = m.k;
+    sid = m.sid;
+    const size_t sv = (size_t)sid * p.n + v;
+    const uint64_t key = p.W[sv];
+    const int32_t lo = p.in_off[v], hi = p.in_off[v + 1];
+    if (key == (((uint64_t)t << 32) | (uint32_t)s0)) {
+      // first marker: CreateLocalSnapshot(src) + SendToNeighbors (node.go:153-156)
+      s_trig[s0 - blockIdx.x * kGThreads] = p.out_off[v + 1] - p.out_off[v];
+      const int slot = atomicAdd(&p.crn[v], 1);
+      p.cre[lo + slot] = ((uint64_t)(uint32_t)s0 << 32) | (uint32_t)sid;
+      if (hi - lo <= kSmallIndeg) {
+        p.stok[sv] = p.tokens[v] - expand_range(p, t, s0, sid, k, lo, hi, 1);
+      } else {
+        p.stok[sv] = p.tokens[v];  // k_push's expansion subtracts the later same-tick tokens
+        bx = BigX{lo, hi, s0, sid, k, v, {0, 0}};
+        bslot = atomicAdd(&s_nb, 1);
+      }
+      const int add = kBig + (hi - lo) - 1;
+      done = atomicAdd(&p.cnt[sv], add) + add == kBig;
+    } else {
+      // later marker: stop recording the channel (node.go:158-160)
+      if ((key >> 32) != (uint64_t)t) {  // created in an earlier tick: cursors exist
+        const uint32_t e = p.chin[k].tokcnt;
+        uint32_t* r = (uint32_t*)&p.rec[(size_t)sid * p.e + k];
+        c[0] += e - r[0];
+        r[1] = e;
+      }  // else created this tick by a lower-ranked sender: its expansion closes it
+      done = atomicAdd(&p.cnt[sv], -1) - 1 == kBig;
+    }
+  }
+  complete_nodes(p, done, sid, t, c[1]);
+  const int idx[2] = {GC_RECORDED, GC_COMPLETED};
+  block_count<2>(p, idx, c);  // (has a barrier: s_trig and s_nb are final below)
+  if (threadIdx.x == 0 && s_nb) s_base = atomicAdd(&p.sc->big_n, s_nb);
+  tally(p, s_trig[threadIdx.x], t);  // (has a barrier: s_base is final below)
+  if (bslot >= 0) p.big[s_base + bslot] = bx;
+}
+
+// Step-0 traffic tally (before the first tick: no triggers).
+__global__ void __launch_bounds__(kGThreads) k_tally(GParams p, int32_t step) {
+  if (block_frozen(p)) return;
+  tally(p, 0, step);
+}
+
+// phase C: exclusive scan of the block tallies (one workgroup, 4 entries per thread),
+// draw bases
 __global__ void __launch_bounds__(1024) k_scan(GParams p) {
-  if (p.sc->status) return;
+  if (block_frozen(p)) return;
   __shared__ long long sh[32];
   long long carry_a = 0, carry_b = 0;
-  for (int c0 = 0; c0 < p.n_blocks; c0 += blockDim.x) {
-    const int i = c0 + threadIdx.x;
-    long long a = i < p.n_blocks ? p.bsum[2 * i] : 0, b = i < p.n_blocks ? p.bsum[2 * i + 1] : 0;
+  for (int c0 = 0; c0 < p.n_pblocks; c0 += 4 * blockDim.x) {
+    const int i0 = c0 + 4 * threadIdx.x;
+    long long va[4], vb[4], a = 0, b = 0;
+    for (int q = 0; q < 4; ++q) {
+      const bool in = i0 + q < p.n_pblocks;
+      va[q] = in ? p.bsum[2 * (i0 + q)] : 0;
+      vb[q] = in ? p.bsum[2 * (i0 + q) + 1] : 0;
+      a += va[q];
+      b += vb[q];
+    }
     long long ta, tb;
     block_exclusive_scan2(a, b, ta, tb, sh);
-    if (i < p.n_blocks) {
-      p.bsum[2 * i] = carry_a + a;
-      p.bsum[2 * i + 1] = carry_b + b;
+    a += carry_a;
+    b += carry_b;
+    for (int q = 0; q < 4; ++q) {
+      if (i0 + q < p.n_pblocks) {
+        p.bsum[2 * (i0 + q)] = a;
+        p.bsum[2 * (i0 + q) + 1] = b;
+      }
+      a += va[q];
+      b += vb[q];
     }
     carry_a += ta;
     carry_b += tb;
@@ -377,16 +398,15 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p) {
   }
 }
 
-// phase F: every node pushes onto its own out-channels -- the broadcasts of the local
-// snapshots created at it this tick (in creating-sender order), then its traffic send.
-__global__ void __launch_bounds__(kThreads) k_push(GParams p, int32_t t, int32_t step) {
-  if (p.sc->status) return;
+// phase D: every node pushes onto its own out-channels -- the broadcasts of the local
+// snapshots created at it this tick (in creating-sender order), then its traffic send;
+// then the grid expands the local snapshots created at high in-degree nodes.
+__global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_t step) {
+  if (block_frozen(p)) return;
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long pushes = 0, peeks = 0;
+  unsigned long long c[2] = {0, 0};  // push, peek
   if (v < p.n) {
     const int32_t ob = p.out_off[v], od = p.out_off[v + 1] - ob;
-    uint64_t mask = p.mask[v];
-    const uint64_t mask0 = mask;
     const int ncre = p.crn[v];
     if (ncre) {
       p.crn[v] = 0;
@@ -403,47 +423,83 @@ __global__ void __launch_bounds__(kThreads) k_push(GParams p, int32_t t, int32_t
         const uint32_t sid = (uint32_t)best;
         if (r == 0 && s0 < v) {
           // The reference delivers s0's marker before v's own turn in this tick, so v's
-          // scan peeks the queues the broadcast made non-empty (sim.go:82-84).
+          // scan peeks the queues the broadcast makes non-empty (sim.go:82-84).
           const int pk = p.pick[v];
           const int pj = (pk >> 6) == t ? (pk & 63) : 64;
           for (int j = 0; j < od && j < pj; ++j)
-            if (!((mask0 >> j) & 1)) ++peeks;
+            if ((uint32_t)p.hq[ob + j] == kEmpty) ++c[1];
         }
-        const unsigned long long draw0 = p.sc->base_trig + (unsigned long long)p.bsum[2 * (s0 / kTallyBlock)] +
+        const unsigned long long draw0 = p.sc->base_trig + (unsigned long long)p.bsum[2 * (s0 / kGThreads)] +
                                          (unsigned long long)p.ltrig[s0];
-        for (int j = 0; j < od; ++j)
-          push_entry(p, ob + j, j, mask, kGMarker | sid, receive_time(p, draw0 + j, t), pushes);
+        for (int j = 0; j < od; ++j) push_entry(p, ob + j, kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
       }
     }
     int32_t j;
     const int32_t tok = p.tokens[v];
     if (traffic_send(p, step, v, od, tok, &j)) {
       // SendTokens(v, out-link j, 1): node.go:112-131
-      const unsigned long long draw = p.sc->base_send + (unsigned long long)p.bsum[2 * (v / kTallyBlock) + 1] +
+      const unsigned long long draw = p.sc->base_send + (unsigned long long)p.bsum[2 * (v / kGThreads) + 1] +
                                       (unsigned long long)p.lsend[v];
       p.tokens[v] = tok - 1;
-      push_entry(p, ob + j, j, mask, 1u, receive_time(p, draw, t), pushes);
+      push_entry(p, ob + j, 1u, receive_time(p, draw, t), c[0]);
     }
-    if (mask != mask0) p.mask[v] = mask;
   }
-  wave_count(&p.sc->push, pushes);
-  wave_count(&p.sc->peek, peeks);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    p.sc->mlist_n = 0;
-    p.sc->xl_n = 0;
+  const int idx[2] = {GC_PUSH, GC_PEEK};
+  block_count<2>(p, idx, c);
+  // expansion of the local snapshots created at high in-degree nodes: the (creation,
+  // in-link) pairs of each staged chunk are numbered by an LDS prefix over in-degrees and
+  // dealt round-robin to every thread of the grid
+  const int nb = p.sc->big_n;
+  constexpr int kChunk = 2 * kGThreads;  // descriptors staged in LDS at a time (16 KB)
+  __shared__ BigX sx[kChunk];
+  __shared__ int32_t spre[kChunk + 1];
+  __shared__ long long ssh[2 * (kGThreads / 64)];
+  const int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+  for (int c0 = 0; c0 < nb; c0 += kChunk) {
+    const int m = nb - c0 < kChunk ? nb - c0 : kChunk;
+    __syncthreads();
+    const int j0 = 2 * threadIdx.x;
+    long long len0 = 0, len1 = 0;
+    if (j0 < m) {
+      sx[j0] = p.big[c0 + j0];
+      len0 = sx[j0].hi - sx[j0].lo;
+    }
+    if (j0 + 1 < m) {
+      sx[j0 + 1] = p.big[c0 + j0 + 1];
+      len1 = sx[j0 + 1].hi - sx[j0 + 1].lo;
+    }
+    long long a = len0 + len1, z = 0, tot, tz;
+    block_exclusive_scan2(a, z, tot, tz, ssh);
+    spre[j0] = (int32_t)a;
+    spre[j0 + 1] = (int32_t)(a + len0);
+    if (threadIdx.x == 0) spre[kChunk] = (int32_t)tot;
+    __syncthreads();
+    for (int64_t w = gt; w < tot; w += gs) {
+      int lo = 0, hi = m - 1;  // last j with spre[j] <= w
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (spre[mid] <= w) lo = mid;
+        else hi = mid - 1;
+      }
+      const BigX x = sx[lo];
+      const int32_t k = x.lo + (int32_t)(w - spre[lo]);
+      const int tsum = expand_range(p, t, x.s0, x.sid, x.karr, k, k + 1, 1);
+      if (tsum) atomicSub(&p.stok[(size_t)x.sid * p.n + x.v], tsum);
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
 // host events of one step, in program order (one workgroup)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_hostops(GParams p, int32_t time, int32_t ob, int32_t oc) {
+__global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, int32_t ob, int32_t oc) {
   __shared__ int s_stop;
+  unsigned long long pushes = 0;
   for (int i = 0; i < oc; ++i) {
     const GOp op = p.ops[ob + i];
     if (threadIdx.x == 0) s_stop = p.sc->status != 0;
     __syncthreads();
-    if (s_stop) return;
+    if (s_stop) break;
     const int32_t v = op.a;
     const int32_t obv = p.out_off[v], od = p.out_off[v + 1] - obv;
     if (op.kind == GOP_SEND) {
@@ -456,18 +512,14 @@ __global__ void __launch_bounds__(kThreads) k_hostops(GParams p, int32_t time, i
           int32_t lo = 0, hi = od;
           while (lo < hi) {
             const int32_t mid = (lo + hi) >> 1;
-            if (p.ch_dst[obv + mid] < op.b) lo = mid + 1;
+            if (p.route[obv + mid].x < op.b) lo = mid + 1;
             else hi = mid;
           }
-          if (op.b < 0 || lo >= od || p.ch_dst[obv + lo] != op.b) {
+          if (op.b < 0 || lo >= od || p.route[obv + lo].x != op.b) {
             set_status(p.sc, ST_FATAL_UNKNOWN_DEST);
           } else {
-            uint64_t mask = p.mask[v];
-            unsigned long long pushes = 0;
             const unsigned long long d = p.sc->draw++;
-            push_entry(p, obv + lo, lo, mask, (uint32_t)op.n, receive_time(p, d, time), pushes);
-            p.mask[v] = mask;
-            p.sc->push += pushes;
+            push_entry(p, obv + lo, (uint32_t)op.n, receive_time(p, d, time), pushes);
           }
         }
       }
@@ -478,24 +530,21 @@ __global__ void __launch_bounds__(kThreads) k_hostops(GParams p, int32_t time, i
       const int32_t lo = p.in_off[v], hi = p.in_off[v + 1];
       uint64_t* rec = p.rec + (size_t)sid * p.e;
       for (int32_t k = lo + (int32_t)threadIdx.x; k < hi; k += blockDim.x)
-        rec[k] = (uint64_t)p.tokcnt[k] | ((uint64_t)kOpen << 32);
+        rec[k] = (uint64_t)p.chin[k].tokcnt | ((uint64_t)kOpen << 32);
       if (threadIdx.x == 0) {
         const size_t sv = (size_t)sid * p.n + v;
         p.W[sv] = ((uint64_t)(uint32_t)time << 32) | 0xffffffffull;
         p.stok[sv] = p.tokens[v];
         atomicAdd(&p.cnt[sv], kBig + (hi - lo));
-        uint64_t mask = p.mask[v];
-        unsigned long long pushes = 0;
         const unsigned long long d = p.sc->draw;
         for (int j = 0; j < od; ++j)
-          push_entry(p, obv + j, j, mask, kGMarker | (uint32_t)sid, receive_time(p, d + j, time), pushes);
+          push_entry(p, obv + j, kGMarker | (uint32_t)sid, receive_time(p, d + j, time), pushes);
         p.sc->draw = d + od;
-        p.mask[v] = mask;
-        p.sc->push += pushes;
       }
     }
     __syncthreads();
   }
+  if (threadIdx.x == 0 && pushes) atomicAdd(&p.cpart[GC_PUSH], pushes);
 }
 
 // ---------------------------------------------------------------------------
@@ -511,7 +560,7 @@ __global__ void k_finish(GParams p, int32_t n_sids, unsigned long long* out) {
     const uint64_t* r = p.rec + (size_t)sid * p.e;
     for (int32_t k = p.in_off[v]; k < p.in_off[v + 1]; ++k) {
       const uint64_t x = r[k];
-      if ((uint32_t)(x >> 32) == kOpen) rec += p.tokcnt[k] - (uint32_t)x;
+      if ((uint32_t)(x >> 32) == kOpen) rec += p.chin[k].tokcnt - (uint32_t)x;
     }
   }
   wave_count(out, rec);
@@ -532,7 +581,7 @@ __global__ void k_checks_state(GParams p, unsigned long long* out) {
   for (size_t v = gt; v < (size_t)p.n; v += gs) fin += (unsigned long long)(long long)p.tokens[v];
   const uint32_t capm = (1u << p.cap_log2) - 1;
   for (size_t c = gt; c < (size_t)p.e; c += gs) {
-    const uint32_t hc = p.hc[c];
+    const uint32_t hc = (uint32_t)(p.hq[c] >> 32);
     for (uint32_t q = 0; q < (hc >> 16); ++q) {
       const uint64_t x = p.fifo[(c << p.cap_log2) + (((hc & 0xffffu) + q) & capm)];
       if (!((uint32_t)x & kGMarker)) infl += (uint32_t)x;
@@ -557,7 +606,7 @@ __global__ void k_checks_snap(GParams p, int32_t n_sids, unsigned long long* out
     }
     const uint64_t* rec = p.rec + (size_t)sid * p.e;
     for (size_t c = gt; c < (size_t)p.e; c += gs) {
-      const int32_t k = p.ch_inpos[c];
+      const int32_t k = p.route[c].y;
       const uint64_t x = rec[k];
       const uint32_t b = (uint32_t)x, e = (uint32_t)(x >> 32);
       const long long s = hist_sum(p, k, b, e);
@@ -576,35 +625,30 @@ inline int grid_for(int64_t n, int threads = kThreads) { return (int)((n + threa
 int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  if ((e = hipMemsetAsync(p.hc, 0, (size_t)p.e * sizeof(uint32_t), s))) return e;
-  if ((e = hipMemsetAsync(p.tokcnt, 0, (size_t)p.e * sizeof(uint32_t), s))) return e;
-  if ((e = hipMemsetAsync(p.deliv, 0, (size_t)p.e * sizeof(uint64_t), s))) return e;
   if ((e = hipMemsetAsync(p.W, 0xff, (size_t)p.s_cap * p.n * sizeof(uint64_t), s))) return e;
   if ((e = hipMemsetAsync(p.cnt, 0, (size_t)p.s_cap * p.n * sizeof(int32_t), s))) return e;
   if ((e = hipMemsetAsync(p.sc, 0, sizeof(GScal), s))) return e;
-  const int64_t m = p.n > p.s_cap ? p.n : p.s_cap;
-  hipLaunchKernelGGL(k_reset_nodes, dim3(grid_for(m)), dim3(kThreads), 0, s, p, init_tok);
+  if ((e = hipMemsetAsync(p.cpart, 0, (size_t)kParts * kNumCnt * sizeof(unsigned long long), s))) return e;
+  int64_t m = p.n > p.e ? p.n : p.e;
+  if (p.s_cap > m) m = p.s_cap;
+  hipLaunchKernelGGL(k_reset, dim3(grid_for(m)), dim3(kThreads), 0, s, p, init_tok);
   return hipGetLastError();
 }
 
 int cg_launch_sends(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_tally, dim3(p.n_blocks), dim3(kThreads), 0, s, p, t);
+  hipLaunchKernelGGL(k_tally, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
-  hipLaunchKernelGGL(k_push, dim3(grid_for(p.n)), dim3(kThreads), 0, s, p, t, t);
+  hipLaunchKernelGGL(k_push, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t, t);
   return hipGetLastError();
 }
 
-int cg_launch_tick(const GParams& p, int32_t t, int32_t lanes_per_creation, void* stream) {
+int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int list_grid = grid_for(p.n) < 2048 ? grid_for(p.n) : 2048;
-  hipLaunchKernelGGL(k_pick, dim3(grid_for(p.n)), dim3(kThreads), 0, s, p, t);
-  hipLaunchKernelGGL(k_marker, dim3(list_grid), dim3(kThreads), 0, s, p, t);
-  const int xg = grid_for((int64_t)p.n * lanes_per_creation);
-  hipLaunchKernelGGL(k_expand, dim3(xg < 4096 ? xg : 4096), dim3(kThreads), 0, s, p, t, lanes_per_creation);
-  hipLaunchKernelGGL(k_tally, dim3(p.n_blocks), dim3(kThreads), 0, s, p, t);
+  hipLaunchKernelGGL(k_pick, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
+  hipLaunchKernelGGL(k_marker, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
-  hipLaunchKernelGGL(k_push, dim3(grid_for(p.n)), dim3(kThreads), 0, s, p, t, t);
+  hipLaunchKernelGGL(k_push, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t, t);
   return hipGetLastError();
 }
 
