@@ -308,10 +308,11 @@ def cpu_baseline_graph(g, cfg, n, steps, snap_steps, snap_nodes, rs, budget_s):
         c = o.counters()
         return secs, c["pop_tok"] + c["pop_mk"], o.status
 
-    probe = min(steps, 8)
-    secs, pk, _ = run(probe)
-    k = int(min(steps, max(probe, probe * budget_s / max(secs, 1e-6))))
+    k = min(steps, 8)
     secs, pk, st = run(k)
+    while secs < budget_s / 3 and k < steps:   # later ticks cost more (longer logs): grow
+        k = min(steps, 2 * k)
+        secs, pk, st = run(k)
     return {"value": pk / secs, "unit": "packets/s", "cores": 1, "kind": "port",
             "sample": f"first {k} of {steps} ticks of the same graph and program ({pk} packets, "
                       f"{secs:.1f} s); CPU restatement in C (oracle/cl_oracle.c), one simulation on one "
