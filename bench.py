@@ -46,7 +46,7 @@ GRAPH_CONFIGS = {
                desc="random 8-out regular digraph, 2^20 nodes, one snapshot under continuous token "
                     "traffic (p=1/4 per node per tick), 80 ticks"),
     "c5": dict(kind="powerlaw", n=100_000, targets=8, exponent=0.9, ring=True, tokens=100, steps=4100,
-               snap_steps=list(range(1, 4097)), fifo=4096, seed=30240,
+               snap_steps=list(range(1, 4097)), fifo=8192, seed=30240,
                desc="power-law digraph (8 Zipf(0.9) targets + ring), 100k nodes, 4,096 overlapping "
                     "snapshots (one start per tick), 4,100-tick window under continuous traffic"),
 }

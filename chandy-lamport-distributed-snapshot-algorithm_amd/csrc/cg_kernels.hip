@@ -255,11 +255,24 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
   unsigned long long c[3] = {0, 0, 0};  // peek, pop_tok, pop_mk
   if (s < p.n) {
     const int32_t base = p.out_off[s], od = p.out_off[s + 1] - base;
-    for (int j = 0; j < od; ++j) {
+    // The first kPre head words are loaded up front as independent loads (one HBM
+    // latency instead of a chain of od); the scan below reads them from registers.
+    constexpr int kPre = 8;
+    uint32_t pre[kPre];
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) pre[j] = j < od ? (uint32_t)p.hq[base + j] : kEmpty;
+    int first = -1;
+#pragma unroll
+    for (int j = 0; j < kPre; ++j) {
+      const bool live = first < 0 && pre[j] != kEmpty;
+      c[0] += live ? 1 : 0;  // Queue.Peek, sim.go:83
+      first = live && pre[j] <= (uint32_t)t ? j : first;
+    }
+    for (int j = first >= 0 ? first : kPre; j < od; ++j) {
       const uint64_t q = p.hq[base + j];
       const uint32_t rt = (uint32_t)q;
       if (rt == kEmpty) continue;
-      ++c[0];  // Queue.Peek, sim.go:83
+      if (j >= kPre) ++c[0];  // Queue.Peek, sim.go:83 (heads past the prefetch)
       if (rt > (uint32_t)t) continue;
       const int32_t ch = base + j;
       const uint32_t hc = (uint32_t)(q >> 32), capm = (1u << p.cap_log2) - 1;
