@@ -12,6 +12,9 @@ enum OpKind : int32_t {
   OP_SNAP = 2,   // a = node rank, b = snapshot id, c = outdeg(a)                   (sim.go:105-123)
   OP_TICK = 3,   // a = number of ticks                                      (sim.go:71-95)
   OP_DRAIN = 4,  // a = max drain ticks, b = extra ticks (maxDelay+1)        (test_common.go:123-137)
+  OP_SENDS = 5,  // a = k: the next k ops are OP_SENDs from pairwise distinct senders, run
+                 // as one lane-parallel step (device program only; built by the host from
+                 // runs of consecutive sends, e.g. one event-file line per node)
 };
 struct Op {
   int32_t kind, a, b, c;

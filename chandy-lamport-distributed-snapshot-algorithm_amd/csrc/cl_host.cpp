@@ -234,7 +234,12 @@ struct cl_sim {
   bool state_valid = false;  // the device state image matches ops[0, executed)
   int64_t layout_row = 0;    // delay row length the LDS layout was sized for
   DevBuf<Op> d_ops;
-  size_t ops_uploaded = 0;
+  // Device program: `ops` with runs of sends from distinct senders folded into OP_SENDS
+  // groups; dmap[i] = device index of logical op i (every launch begins at a group start).
+  std::vector<Op> dops;
+  std::vector<int32_t> dmap;
+  size_t dops_for = 0;
+  int32_t dops_begin = -1;
   DevBuf<uint32_t> d_topo;
   DevBuf<int32_t> d_fin_tok;
   DevBuf<uint8_t> d_sched;
@@ -468,11 +473,41 @@ struct cl_sim {
     return CL_OK;
   }
 
+  // Fold every maximal run of consecutive sends with pairwise distinct senders (and not
+  // crossing the launch start `begin`) into one OP_SENDS group.  Within such a run no send
+  // changes another's sender balance or channel, so the kernel can run them in parallel
+  // lanes with draw k + position (the reference's draw order, sim.go:101).
+  void build_device_program(int32_t begin) {
+    dops.clear();
+    dmap.assign(ops.size() + 1, 0);
+    size_t i = 0;
+    while (i < ops.size()) {
+      size_t j = i + 1;
+      if (ops[i].kind == OP_SEND) {
+        uint64_t seen = 1ull << ops[i].a;
+        while (j < ops.size() && ops[j].kind == OP_SEND && (int64_t)j != begin && !((seen >> ops[j].a) & 1ull)) {
+          seen |= 1ull << ops[j].a;
+          ++j;
+        }
+      }
+      if (j - i >= 2) {
+        for (size_t k = i; k < j; ++k) dmap[k] = (int32_t)dops.size();
+        dops.push_back(Op{OP_SENDS, (int32_t)(j - i), 0, 0});
+        dops.insert(dops.end(), ops.begin() + i, ops.begin() + j);
+      } else {
+        dmap[i] = (int32_t)dops.size();
+        dops.push_back(ops[i]);
+      }
+      i = j;
+    }
+    dmap[ops.size()] = (int32_t)dops.size();
+  }
+
   ExecParams exec_params(int32_t op_begin, int32_t n_started_before) const {
     ExecParams p{};
     const int n = (int)ids.size(), C = (int)ch_dst.size();
-    p.op_begin = op_begin;
-    p.op_end = (int32_t)ops.size();
+    p.op_begin = dmap[op_begin];
+    p.op_end = (int32_t)dops.size();
     p.n_nodes = n;
     p.n_ch = C;
     p.lay = lay;
@@ -508,12 +543,14 @@ struct cl_sim {
                      (long long)layout_row);
     if (force_fresh || !state_valid) need_fresh = true;
     if (!need_fresh && executed == (int32_t)ops.size()) return CL_OK;
-    if (ops.size() > ops_uploaded || !d_ops.p) {
-      if ((rc = d_ops.ensure(std::max<size_t>(ops.size(), 64)))) return rc;
-      HIP_TRY(hipMemcpy(d_ops.p, ops.data(), ops.size() * sizeof(Op), hipMemcpyHostToDevice));
-      ops_uploaded = ops.size();
-    }
     int32_t begin = need_fresh ? 0 : executed;
+    if (ops.size() != dops_for || begin != dops_begin || !d_ops.p) {
+      build_device_program(begin);
+      if ((rc = d_ops.ensure(std::max<size_t>(dops.size(), 64)))) return rc;
+      HIP_TRY(hipMemcpy(d_ops.p, dops.data(), dops.size() * sizeof(Op), hipMemcpyHostToDevice));
+      dops_for = ops.size();
+      dops_begin = begin;
+    }
     int32_t started_before = 0;
     for (int32_t i = 0; i < begin; ++i) started_before += ops[i].kind == OP_SNAP;
     if (begin == 0) {

@@ -33,6 +33,17 @@
 #include "cl_engine.h"
 
 namespace clsnap {
+
+#if CLSNAP_PROF
+// Diagnostic build (make variant NAME=prof DEFS=-DCLSNAP_PROF=1): shader-clock cycles per
+// program part, summed over waves.  [0] SEND ops, [1] SNAP ops, [2] tick phase A+B,
+// [3] tick phase C/D, [4] drain/tick loop control, [5] prologue, [6] epilogue, [7] ticks.
+__device__ unsigned long long g_prof[8];
+#define PROF_T() ((unsigned long long)__builtin_readcyclecounter())
+#else
+#define PROF_T() 0ull
+#endif
+
 namespace {
 
 // LDS pointers carry their address space explicitly: a generic pointer lets the compiler
@@ -63,7 +74,15 @@ struct Lane {
   uint32_t peek, pop_tok, pop_mk, push;
   bool alive;    // instance still running (uniform within the segment)
   int32_t flag;  // lane-local engine failure raised during an op/tick
+#if CLSNAP_PROF
+  unsigned long long prof[8];
+#endif
 };
+#if CLSNAP_PROF
+#define PROF_ADD(ln, k, t0) ((ln).prof[k] += PROF_T() - (t0))
+#else
+#define PROF_ADD(ln, k, t0) ((void)(t0))
+#endif
 
 // Small degree bounds keep loops unrolled and predicated with the in-link words in
 // registers; larger ones use compact runtime loops over the node's own degree with the
@@ -114,14 +133,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 }
 
 // Queue.Push (queue.go:18-20) on out-link ko; receiveTime = time + 1 + draw (sim.go:101).
-// `k` is the index of the draw in this instance's delay stream.
+// `k` is the index of the draw in this instance's delay stream.  STAGED: the wave's delay rows
+// are staged in LDS.  A compile-time choice: with an HBM delay load anywhere on the path
+// the compiler waits with s_waitcnt vmcnt(0) at the join, and on gfx950 vmcnt also counts
+// the wave's outstanding global STORES (snapshot outputs) -- a full store drain per push.
+template <bool STAGED>
 __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int64_t k) {
   const Layout& lay = x.lay;
   if (k >= x.p.draws) { ln.flag = ST_DELAY_EXHAUSTED; return; }
   const uint32_t chw = PW(lay.w_chw + ko);
   const uint32_t cnt = (chw >> 8) & 0xffu;
   if (cnt >= (uint32_t)kMaxQueued) { ln.flag = ST_FIFO_OVERFLOW; return; }
-  const uint32_t delay = x.lrow ? x.lrow[k] : x.sched[(size_t)x.inst * x.p.sched_row + k];
+  uint32_t delay;
+  if constexpr (STAGED) delay = x.lrow[k];
+  else delay = x.sched[(size_t)x.inst * x.p.sched_row + k];
   const uint32_t e = payload | ((uint32_t)(ln.time + 1 + (int32_t)delay) << 16);
   const uint32_t cap = 1u << lay.cap_log2;
   if (__builtin_expect(cnt < cap, 1)) {
@@ -238,10 +263,11 @@ __device__ __forceinline__ void refill(const Ctx& x, int32_t ko, uint32_t slot) 
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
 // Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
 // it[] holds this node's in-link words.
-template <int D>
+template <int D, bool STAGED>
 __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
+  const unsigned long long pt0 = PROF_T();
   ln.time += act ? 1 : 0;
   // ---- A: pick ------------------------------------------------------------
   uint32_t pick = 0, empty_scanned = 0;
@@ -332,6 +358,8 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
     }
   }
   // ---- C/D: broadcast draws in sender order, then push -------------------------
+  const unsigned long long pt1 = PROF_T();
+  PROF_ADD(ln, 2, pt0);
   if (__ballot(ntrig > 0)) {
     wave_sync();
     const uint32_t t = XW(lay.x_tslot + x.lane);
@@ -349,7 +377,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
 #pragma unroll
       for (int32_t j = 0; j < D; ++j) {
         if (j >= x.outdeg) continue;
-        push(x, ln, j, kMarkerBit | sid, k0 + j);
+        push<STAGED>(x, ln, j, kMarkerBit | sid, k0 + j);
         // the reference scans this sender's links after the push when the trigger came
         // from a lower rank: a link that was empty at tick start gets peeked once more
         if ((int32_t)src < x.v && ((empty_scanned >> j) & 1u)) {
@@ -361,6 +389,76 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
     ln.draw += act ? (int32_t)total : 0;
   }
   resolve_failures(x, ln);
+  PROF_ADD(ln, 3, pt1);
+#if CLSNAP_PROF
+  ln.prof[7] += 1;
+#endif
+}
+
+// SendTokens (node.go:112-131) of one send event: balance check, link lookup, push -- all
+// at the sender.  Must be reached by all lanes of the wave.
+template <int D, bool STAGED>
+__device__ __forceinline__ void send_one(const Ctx& x, Lane& ln, const Op& op) {
+  const bool me = ln.alive && x.v == op.a;
+  const bool insufficient = me && ln.tokens < op.c;
+  const bool fatal = ((__ballot(insufficient) >> (x.seg_base + op.a)) & 1ull) != 0;
+  if (me && !insufficient && op.b >= 0) {
+    ln.tokens -= op.c;
+#pragma unroll
+    for (int32_t j = 0; j < D; ++j)  // static register indices for the out-link
+      if (j == op.b) push<STAGED>(x, ln, j, (uint32_t)op.c, ln.draw);
+  }
+  if (ln.alive) {
+    if (fatal) {
+      ln.status = ST_FATAL_INSUFFICIENT;
+      ln.alive = false;
+    } else if (op.b < 0) {
+      ln.status = ST_FATAL_UNKNOWN_DEST;
+      ln.alive = false;
+    } else {
+      ln.draw += 1;
+    }
+  }
+  resolve_failures(x, ln);
+}
+
+// A group of k send events with pairwise distinct senders (OP_SENDS): no event changes
+// another's sender balance or channel, so when none of them fails every sender lane runs
+// its own event at once, with draw index draw + its position in the group.  If any event
+// of the wave would fail, the events run one by one (send_one), which freezes an instance
+// exactly where the sequential program does.
+template <int D, bool STAGED>
+__device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __restrict__ ev, int32_t k) {
+  const Layout& lay = x.lay;
+  int32_t pos = -1, oj = 0, on = 0;
+  for (int32_t q = 0; q < k; ++q) {
+    const Op s = ev[q];
+    const bool me = x.v == s.a;
+    pos = me ? q : pos;
+    oj = me ? s.b : oj;
+    on = me ? s.c : on;
+  }
+  const bool mine = ln.alive && pos >= 0;
+  bool bad = false;
+  if (mine) {
+    if (ln.tokens < on || oj < 0 || (int64_t)ln.draw + pos >= x.p.draws) {
+      bad = true;
+    } else {  // the checks push() makes
+      const uint32_t cnt = (PW(lay.w_chw + oj) >> 8) & 0xffu, cap = 1u << lay.cap_log2;
+      bad = cnt >= (uint32_t)kMaxQueued || (cnt >= cap && (lay.ocap_log2 < 0 || cnt - cap >= (1u << lay.ocap_log2)));
+    }
+  }
+  if (__builtin_expect(__ballot(bad) != 0, 0)) {
+    for (int32_t q = 0; q < k; ++q) send_one<D, STAGED>(x, ln, ev[q]);
+    return;
+  }
+  if (mine) {
+    ln.tokens -= on;
+#pragma unroll
+    for (int32_t j = 0; j < D; ++j)
+      if (j == oj) push<STAGED>(x, ln, j, (uint32_t)on, (int64_t)ln.draw + pos);
+  }
+  if (ln.alive) ln.draw += k;
 }
 
 // Occupancy target per degree bound (waves per SIMD; 256-thread workgroups).  Forcing
@@ -379,7 +477,7 @@ constexpr int waves_for(int D) {
   return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1) : D == 4 ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : 1;
 }
 
-template <int D>
+template <int D, bool STAGED>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
                                                                          const Op* __restrict__ ops,
                                                                          const uint8_t* __restrict__ sched) {
@@ -400,9 +498,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   const int32_t outdeg = valid ? (int32_t)nb[1] : 0;
   const uint32_t st = (uint32_t)p.stride;
   // Stage the wave's delay rows (ipw contiguous rows of sched_row bytes) in LDS when they fit.
-  const bool staged = lay.x_delay > 0;
-  const lds_u8* lrow = staged ? (const lds_u8*)(X + lay.x_delay) + (size_t)seg * p.sched_row : nullptr;
-  if (staged) {
+  const lds_u8* lrow = STAGED ? (const lds_u8*)(X + lay.x_delay) + (size_t)seg * p.sched_row : nullptr;
+  if constexpr (STAGED) {
     const uint32_t first = wave * (uint32_t)lay.ipw;
     const uint32_t nrow = min((uint32_t)lay.ipw, (uint32_t)p.n_inst - min(first, (uint32_t)p.n_inst));
     const uint32_t words = nrow * (uint32_t)(p.sched_row / 4);
@@ -421,6 +518,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
 
   Lane ln;
   ln.flag = 0;
+#if CLSNAP_PROF
+  for (int k = 0; k < 8; ++k) ln.prof[k] = 0;
+  const unsigned long long pro0 = PROF_T();
+#endif
   for (int32_t k = lane; k < lay.x_delay_begin; k += kWave) XW(lay.priv * kWave + k) = 0u;
   if (p.fresh) {
     for (int32_t k = 0; k < lay.priv; ++k) PW(k) = 0u;
@@ -454,32 +555,20 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   wave_sync();
   ln.alive = valid && ln.status == ST_OK;
   int32_t n_started = p.n_started_before;
+#if CLSNAP_PROF
+  PROF_ADD(ln, 5, pro0);
+#endif
 
   for (int32_t i = p.op_begin; i < p.op_end; ++i) {
     const Op op = ops[i];
+    const unsigned long long ot0 = PROF_T();
     if (op.kind == OP_SEND) {
-      // SendTokens (node.go:112-131): balance check, link lookup, push -- all at src
-      const bool me = ln.alive && v == op.a;
-      const bool insufficient = me && ln.tokens < op.c;
-      const bool fatal = ((__ballot(insufficient) >> (x.seg_base + op.a)) & 1ull) != 0;
-      if (me && !insufficient && op.b >= 0) {
-        ln.tokens -= op.c;
-#pragma unroll
-        for (int32_t j = 0; j < D; ++j)  // static register indices for the out-link
-          if (j == op.b) push(x, ln, j, (uint32_t)op.c, ln.draw);
-      }
-      if (ln.alive) {
-        if (fatal) {
-          ln.status = ST_FATAL_INSUFFICIENT;
-          ln.alive = false;
-        } else if (op.b < 0) {
-          ln.status = ST_FATAL_UNKNOWN_DEST;
-          ln.alive = false;
-        } else {
-          ln.draw += 1;
-        }
-      }
-      resolve_failures(x, ln);
+      send_one<D, STAGED>(x, ln, op);
+      PROF_ADD(ln, 0, ot0);
+    } else if (op.kind == OP_SENDS) {
+      send_group<D, STAGED>(x, ln, ops + i + 1, op.a);
+      i += op.a;
+      PROF_ADD(ln, 0, ot0);
     } else if (op.kind == OP_SNAP) {
       // sim.StartSnapshot -> node.StartSnapshot: the initiator records every in-channel
       if (ln.alive && v == op.a) {
@@ -489,11 +578,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
         PW(pi) = (PW(pi) & ~(0xffu << sh)) | ((uint32_t)indeg << sh);
 #pragma unroll
         for (int32_t j = 0; j < D; ++j)
-          if (j < outdeg) push(x, ln, j, kMarkerBit | (uint32_t)op.b, (int64_t)ln.draw + j);
+          if (j < outdeg) push<STAGED>(x, ln, j, kMarkerBit | (uint32_t)op.b, (int64_t)ln.draw + j);
       }
       if (ln.alive) ln.draw += op.c;
       n_started++;
       resolve_failures(x, ln);
+      PROF_ADD(ln, 1, ot0);
     } else if (op.kind == OP_TICK || op.kind == OP_DRAIN) {
       // TICK: op.a ticks.  DRAIN: tick until every started snapshot completed (at most
       // op.a ticks, else HANG), then op.b more (test_common.go:123-137).  Per instance.
@@ -509,11 +599,17 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
         }
         const bool act = ln.alive && (waiting || rem > 0);
         if (!__ballot(act)) break;
-        tick<D>(x, ln, it, act);
+        tick<D, STAGED>(x, ln, it, act);
         rem -= (act && !waiting) ? 1 : 0;
       }
+#if CLSNAP_PROF
+      PROF_ADD(ln, 4, ot0);
+#endif
     }
   }
+#if CLSNAP_PROF
+  const unsigned long long epi0 = PROF_T();
+#endif
 
   // ---- epilogue: tokens still queued, per-instance sums, outputs, state image ------
   int32_t inflight = 0;
@@ -546,6 +642,13 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     lds_add(acc + 4, (uint32_t)inflight);
   }
   wave_sync();
+#if CLSNAP_PROF
+  PROF_ADD(ln, 6, epi0);
+  if (lane == 0) {
+    ln.prof[4] -= ln.prof[2] + ln.prof[3];  // loop control only
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_prof[k], ln.prof[k]);
+  }
+#endif
   if (!valid) return;
   p.fin_tok[ii * (uint32_t)N + v] = ln.tokens;
   if (v == 0) {
@@ -639,19 +742,25 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
 
 }  // namespace
 
-template <int D>
-int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
+template <int D, bool STAGED>
+int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
   const size_t lds = (size_t)p.lay.wave_words * kWavesPerBlock * sizeof(uint32_t);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
   const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
   const unsigned blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL(cl_exec_kernel<D>, dim3(blocks), dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, p,
+  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED>), dim3(blocks), dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, p,
                      topo, ops, sched);
   return (int)hipGetLastError();
+}
+
+template <int D>
+int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
+  return p.lay.x_delay > 0 ? launch_exec_ds<D, true>(p, topo, ops, sched, stream)
+                           : launch_exec_ds<D, false>(p, topo, ops, sched, stream);
 }
 
 // The kernel is instantiated for degree bounds 1, 2, 4, ... CLSNAP_MAX_D.
@@ -670,6 +779,17 @@ int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const 
   return (int)hipErrorNotSupported;
 #endif
 }
+
+#if CLSNAP_PROF
+extern "C" int cl_prof_read(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof));
+  if (e == hipSuccess && reset) {
+    static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
 
 int launch_checksums(const SumParams& p, void* stream) {
   const unsigned blocks = (unsigned)((p.n_inst + 255) / 256);
