@@ -201,3 +201,36 @@ def test_random_scenarios(seed):
     for i in range(n):
         compare_instance(sim, i, oracle_run(top, events, seed=O.REFERENCE_SEED + i),
                          status=status, times=times)
+
+
+@pytest.mark.parametrize("seed,tlo,thi", [(0, 4, 8), (3, 4, 8), (1, 3, 7), (2, 3, 7)])
+def test_send_groups_with_midgroup_fatals(seed, tlo, thi):
+    """Event lines of sends from distinct senders run as one lane-parallel group
+    (OP_SENDS).  Low balances make delay-dependent insufficient-token fatals land in the
+    middle of groups (about 40% of the instances): every instance must freeze exactly
+    where the sequential reference does (status and frozen node balances), and OK
+    instances must match exactly."""
+    rng = np.random.default_rng(500 + seed)
+    n_nodes = int(rng.integers(3, 12))
+    ids = [f"N{k}" for k in range(1, n_nodes + 1)]
+    top = f"{n_nodes}\n" + "".join(f"{i} {int(rng.integers(tlo, thi))}\n" for i in ids)
+    top += "".join(f"{ids[k]} {ids[(k + 1) % n_nodes]}\n{ids[k]} {ids[(k - 1) % n_nodes]}\n"
+                   for k in range(n_nodes))
+    ev = []
+    for r in range(12):
+        order = rng.permutation(n_nodes)
+        for k in order[: int(rng.integers(2, n_nodes + 1))]:
+            ev.append(f"send {ids[k]} {ids[(k + int(rng.integers(0, 2)) * 2 - 1) % n_nodes]} 1")
+        if r % 3 == 0:
+            ev.append(f"snapshot {ids[int(rng.integers(0, n_nodes))]}")
+        ev.append("tick 3")
+    events = "\n".join(ev) + "\n"
+    n = 256
+    sim = engine_run(top, events, n)
+    status, times = sim.status(), sim.time()
+    assert (status == cl.INST_FATAL_INSUFFICIENT_TOKENS).any() and (status == cl.INST_OK).any()
+    for i in range(n):
+        ref = oracle_run(top, events, seed=O.REFERENCE_SEED + i)
+        compare_instance(sim, i, ref, status=status, times=times)
+        if status[i] == cl.INST_FATAL_INSUFFICIENT_TOKENS:
+            assert sim.node_tokens(i) == ref.node_tokens(), f"instance {i}: frozen balances differ"
