@@ -198,3 +198,30 @@ def test_c4_full_size_properties():
     g.rerun()
     g.synchronize()
     assert g.checksums() == sums
+
+
+def test_c5_full_size_properties():
+    """BASELINE config 5 at full size: 100k-node power-law digraph (8 Zipf(0.9) targets
+    + ring), one snapshot start per tick for 4,096 ticks under continuous traffic,
+    4,100 ticks.  Head-of-line scanning in dest order (sim.go:76-90) starves a busy
+    sender's higher links, so channels hold up to all 4,096 markers (8,192 slots)."""
+    n, steps, snaps = 100_000, 4100, 4096
+    g = clg.GraphSim(fifo_slots=8192, max_snapshots=snaps)
+    g.generate_powerlaw(n, 8, 0.9, True, 100, seed=30240)
+    g.set_delay_hash(30241)
+    g.set_traffic(30242, 1 << 30, steps)
+    for k in range(steps):
+        if 1 <= k <= snaps:
+            g.start_snapshot_rank(G.mulhi(G.counter_hash(30243, k - 1, 1), n))
+        g.Tick(1)
+    g.flush()
+    assert g.status() == 0
+    sums = g.checksums()
+    assert sums["final_residual"] == 0 and sums["cut_residual"] == 0
+    c = g.counters()
+    assert c["pop_mk"] <= snaps * g.num_channels
+    assert c["pop_tok"] + c["pop_mk"] == sums["delivered"]
+    assert c["push"] >= sums["delivered"]
+    g.rerun()
+    g.synchronize()
+    assert g.checksums() == sums
