@@ -331,7 +331,7 @@ def cpu_baseline(top, events, n_total, budget_s):
     secs, st, _, cnt, _ = O.run_batch(t_text, e_text, probe, threads=threads)
     sample = int(min(n_total, max(probe, probe / max(secs, 1e-6) * budget_s)))
     total_s, total_pkts, passes = 0.0, 0, 0
-    while passes == 0 or total_s < 0.5 * budget_s:
+    while passes == 0 or total_s < budget_s:
         secs, st, _, cnt, _ = O.run_batch(t_text, e_text, sample, threads=threads)
         ok = st == 0
         total_pkts += int((cnt[ok, 2] + cnt[ok, 3]).sum())
