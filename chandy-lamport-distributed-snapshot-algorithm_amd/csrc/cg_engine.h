@@ -131,7 +131,8 @@ struct GParams {
   int32_t* cnt;        // [s_cap * n] pending accumulator
   int32_t* stok;       // [s_cap * n] recorded node tokens
   uint64_t* rec;       // [s_cap * e] by in-position: recording cursors
-  int32_t* done;       // [s_cap] nodes complete
+  int32_t* done;       // [s_cap] node groups complete (p.done[s_cap..] = gdone)
+  int32_t* gdone;      // [s_cap * n_pblocks] nodes complete per group of kGThreads ranks
   int32_t* ctick;      // [s_cap] completion tick (-1)
   GScal* sc;
   const GOp* ops;

@@ -401,7 +401,7 @@ struct cl_graph {
         (rc = d_chin.ensure(E)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
         (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_W.ensure(s_cap * N)) ||
         (rc = d_rec.ensure(s_cap * E)) || (rc = d_cnt.ensure(s_cap * N)) || (rc = d_stok.ensure(s_cap * N)) ||
-        (rc = d_done.ensure(s_cap)) || (rc = d_ctick.ensure(s_cap)) || (rc = d_sc.ensure(1)) ||
+        (rc = d_done.ensure((size_t)s_cap * (1 + NP))) || (rc = d_ctick.ensure(s_cap)) || (rc = d_sc.ensure(1)) ||
         (rc = d_scratch.ensure(3 + (size_t)s_cap)))
       return rc;
     return CL_OK;
@@ -466,6 +466,7 @@ struct cl_graph {
     p.stok = d_stok.p;
     p.rec = d_rec.p;
     p.done = d_done.p;
+    p.gdone = d_done.p + s_cap;
     p.ctick = d_ctick.p;
     p.sc = d_sc.p;
     p.ops = d_ops.p;

@@ -121,23 +121,21 @@ __device__ inline bool traffic_send(const GParams& p, int64_t step, int32_t v, i
   return true;
 }
 
-// NotifyCompletedSnapshot (sim.go:126-131) for every lane with `done`: one atomic per
-// distinct snapshot id in the wave; the add that reaches N completes the snapshot.
-__device__ inline void complete_nodes(const GParams& p, bool done, int32_t sid, int32_t t,
+// NotifyCompletedSnapshot (sim.go:126-131) for every lane with `done` (node v complete
+// in snapshot sid).  Two-level count, so no word sees more than a few hundred atomics: a
+// node completes its group of kGThreads node ranks, the group that fills completes one
+// of the snapshot's n_pblocks groups, and the add that fills the last one completes the
+// snapshot (one word per snapshot hit by every completing wave serialized a whole tick
+// behind it: ~16k same-address atomics at ~11 ns when a C4 snapshot sweeps the graph).
+__device__ inline void complete_nodes(const GParams& p, bool done, int32_t sid, int32_t v, int32_t t,
                                       unsigned long long& completed) {
-  uint64_t m = __ballot(done);
-  while (m) {
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    const int32_t lsid = __shfl(sid, leader);
-    const uint64_t same = __ballot(done && sid == lsid);
-    if ((int)lane_id() == leader) {
-      const int c = (int)__popcll(same);
-      if (atomicAdd(&p.done[lsid], c) + c == p.n) {
-        p.ctick[lsid] = t;
-        ++completed;
-      }
-    }
-    m &= ~same;
+  if (!done) return;
+  const int32_t g = v / kGThreads;
+  const int32_t gsize = min(kGThreads, p.n - g * kGThreads);
+  if (atomicAdd(&p.gdone[(size_t)sid * p.n_pblocks + g], 1) + 1 != gsize) return;
+  if (atomicAdd(&p.done[sid], 1) + 1 == p.n_pblocks) {
+    p.ctick[sid] = t;
+    ++completed;
   }
 }
 
@@ -233,10 +231,7 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
     p.chin[i] = ChIn{0u, 0u, 0u, p.in_src[i]};
     p.hq[i] = kEmpty;
   }
-  if (i < (size_t)p.s_cap) {
-    p.done[i] = 0;
-    p.ctick[i] = -1;
-  }
+  if (i < (size_t)p.s_cap) p.ctick[i] = -1;
 }
 
 // ---------------------------------------------------------------------------
@@ -317,19 +312,28 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t t) {
   if (block_frozen(p)) return;
   __shared__ int s_nb, s_base;
   __shared__ int s_trig[kGThreads];
+  // local snapshots created by this block's markers at nodes of in-degree <= kSmallIndeg,
+  // expanded over their in-links by the whole block: (creation, in-link) pairs are
+  // numbered by an exclusive prefix over the in-degrees
+  __shared__ BigX s_cx[kGThreads];
+  __shared__ int32_t s_cpre[kGThreads];
+  __shared__ int32_t s_ctsum[kGThreads];
+  __shared__ long long s_sh[2 * (kGThreads / 64)];
   s_trig[threadIdx.x] = 0;
+  s_ctsum[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_nb = 0;
   __syncthreads();
   const int nm = p.mcnt[blockIdx.x];
   unsigned long long c[2] = {0, 0};  // recorded, completed
   bool done = false;
-  int32_t sid = 0;
-  int bslot = -1;
+  int32_t sid = 0, vdone = 0;
+  int bslot = -1, cslot = -1;
   BigX bx;
   if ((int)threadIdx.x < nm) {
     const MDel m = p.mlist[blockIdx.x * kGThreads + threadIdx.x];
     const int32_t s0 = m.s0, v = m.v, k = m.k;
     sid = m.sid;
+    vdone = v;
     const size_t sv = (size_t)sid * p.n + v;
     const uint64_t key = p.W[sv];
     const int32_t lo = p.in_off[v], hi = p.in_off[v + 1];
@@ -338,11 +342,11 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t t) {
       s_trig[s0 - blockIdx.x * kGThreads] = p.out_off[v + 1] - p.out_off[v];
       const int slot = atomicAdd(&p.crn[v], 1);
       p.cre[lo + slot] = ((uint64_t)(uint32_t)s0 << 32) | (uint32_t)sid;
+      bx = BigX{lo, hi, s0, sid, k, v, {0, 0}};
       if (hi - lo <= kSmallIndeg) {
-        p.stok[sv] = p.tokens[v] - expand_range(p, t, s0, sid, k, lo, hi, 1);
+        cslot = 0;  // numbered below
       } else {
         p.stok[sv] = p.tokens[v];  // k_push's expansion subtracts the later same-tick tokens
-        bx = BigX{lo, hi, s0, sid, k, v, {0, 0}};
         bslot = atomicAdd(&s_nb, 1);
       }
       const int add = kBig + (hi - lo) - 1;
@@ -358,9 +362,33 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t t) {
       done = atomicAdd(&p.cnt[sv], -1) - 1 == kBig;
     }
   }
-  complete_nodes(p, done, sid, t, c[1]);
+  complete_nodes(p, done, sid, vdone, t, c[1]);
   const int idx[2] = {GC_RECORDED, GC_COMPLETED};
   block_count<2>(p, idx, c);  // (has a barrier: s_trig and s_nb are final below)
+  // creations numbered in thread order (b), in-link pairs by the prefix of in-degrees (a)
+  const bool cre = cslot >= 0;
+  long long a = cre ? (long long)(bx.hi - bx.lo) : 0, b = cre ? 1 : 0, tot, nc;
+  block_exclusive_scan2(a, b, tot, nc, s_sh);
+  if (cre) {
+    cslot = (int)b;
+    s_cx[cslot] = bx;
+    s_cpre[cslot] = (int32_t)a;
+  }
+  __syncthreads();
+  for (int32_t w = threadIdx.x; w < (int32_t)tot; w += kGThreads) {
+    int lo = 0, hi = (int)nc - 1;  // last creation j with s_cpre[j] <= w
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_cpre[mid] <= w) lo = mid;
+      else hi = mid - 1;
+    }
+    const BigX& x = s_cx[lo];
+    const int32_t kk = x.lo + (w - s_cpre[lo]);
+    const int ts = expand_range(p, t, x.s0, x.sid, x.karr, kk, kk + 1, 1);
+    if (ts) atomicAdd(&s_ctsum[lo], ts);
+  }
+  __syncthreads();
+  if (cslot >= 0) p.stok[(size_t)bx.sid * p.n + bx.v] = p.tokens[bx.v] - s_ctsum[cslot];
   if (threadIdx.x == 0 && s_nb) s_base = atomicAdd(&p.sc->big_n, s_nb);
   tally(p, s_trig[threadIdx.x], t);  // (has a barrier: s_base is final below)
   if (bslot >= 0) p.big[s_base + bslot] = bx;
@@ -411,6 +439,88 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p) {
   }
 }
 
+// The r-th local snapshot created at v this tick in creating-sender order (prev = the
+// (r-1)-th): selection over the node's creation slots.
+__device__ inline uint64_t next_creation(const GParams& p, int32_t lo, int ncre, int r, uint64_t prev) {
+  uint64_t best = ~0ull;
+  for (int i = 0; i < ncre; ++i) {
+    const uint64_t x = p.cre[lo + i];
+    if ((r == 0 || x > prev) && x < best) best = x;
+  }
+  return best;
+}
+
+// First draw index of the broadcast triggered by sender s0's delivery this tick, and of
+// v's traffic send (the scan kernel's block offsets + block-local prefixes).
+__device__ inline unsigned long long broadcast_draw(const GParams& p, int32_t s0) {
+  return p.sc->base_trig + (unsigned long long)p.bsum[2 * (s0 / kGThreads)] + (unsigned long long)p.ltrig[s0];
+}
+__device__ inline unsigned long long send_draw(const GParams& p, int32_t v) {
+  return p.sc->base_send + (unsigned long long)p.bsum[2 * (v / kGThreads) + 1] + (unsigned long long)p.lsend[v];
+}
+
+// Queue.Push onto a channel whose head word q is held in a register.
+__device__ inline void push_q(const GParams& p, int32_t c, uint64_t& q, uint32_t payload, uint32_t rt,
+                              unsigned long long& pushes) {
+  const uint32_t hc = (uint32_t)(q >> 32);
+  const uint32_t head = hc & 0xffffu, cnt = hc >> 16, cap = 1u << p.cap_log2;
+  if (cnt >= cap) {
+    set_status(p.sc, ST_FIFO_OVERFLOW);
+    return;
+  }
+  p.fifo[((size_t)c << p.cap_log2) + ((head + cnt) & (cap - 1))] = ((uint64_t)rt << 32) | payload;
+  q = ((uint64_t)(head | ((cnt + 1) << 16)) << 32) | (cnt == 0 ? rt : (uint32_t)q);
+  ++pushes;
+}
+
+// k_push for a node of out-degree <= kRegOd with local snapshots created this tick: the node's head words are loaded once as
+// independent loads, every push of the tick (broadcasts in creating-sender order, then
+// the traffic send) updates them in registers, and they are stored once.
+constexpr int kRegOd = 16;
+template <int R>
+__device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int32_t ob, int32_t od, int ncre,
+                                     bool send, int32_t tok, int32_t tj, unsigned long long (&c)[2]) {
+  uint64_t q[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) q[j] = j < od ? p.hq[ob + j] : 0ull;
+  if (ncre) {
+    p.crn[v] = 0;
+    const int32_t lo = p.in_off[v];
+    uint64_t prev = 0;
+    for (int r = 0; r < ncre; ++r) {
+      const uint64_t best = next_creation(p, lo, ncre, r, prev);
+      prev = best;
+      const int32_t s0 = (int32_t)(best >> 32);
+      const uint32_t sid = (uint32_t)best;
+      if (r == 0 && s0 < v) {
+        // The reference delivers s0's marker before v's own turn in this tick, so v's
+        // scan peeks the queues the broadcast makes non-empty (sim.go:82-84).
+        const int pk = p.pick[v];
+        const int pj = (pk >> 6) == t ? (pk & 63) : 64;
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if (j < od && j < pj && (uint32_t)q[j] == kEmpty) ++c[1];
+      }
+      const unsigned long long draw0 = broadcast_draw(p, s0);
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (j < od) push_q(p, ob + j, q[j], kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
+    }
+  }
+  if (send) {
+    // SendTokens(v, out-link tj, 1): node.go:112-131
+    p.tokens[v] = tok - 1;
+    const uint32_t rt = receive_time(p, send_draw(p, v), t);
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+      if (j == tj) push_q(p, ob + j, q[j], 1u, rt, c[0]);
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (j < od && (ncre || j == tj)) p.hq[ob + j] = q[j];
+  }
+}
+
 // phase D: every node pushes onto its own out-channels -- the broadcasts of the local
 // snapshots created at it this tick (in creating-sender order), then its traffic send;
 // then the grid expands the local snapshots created at high in-degree nodes.
@@ -421,40 +531,39 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_
   if (v < p.n) {
     const int32_t ob = p.out_off[v], od = p.out_off[v + 1] - ob;
     const int ncre = p.crn[v];
-    if (ncre) {
-      p.crn[v] = 0;
-      const int32_t lo = p.in_off[v];
-      uint64_t prev = 0;
-      for (int r = 0; r < ncre; ++r) {
-        uint64_t best = ~0ull;
-        for (int i = 0; i < ncre; ++i) {
-          const uint64_t x = p.cre[lo + i];
-          if ((r == 0 || x > prev) && x < best) best = x;
-        }
-        prev = best;
-        const int32_t s0 = (int32_t)(best >> 32);
-        const uint32_t sid = (uint32_t)best;
-        if (r == 0 && s0 < v) {
-          // The reference delivers s0's marker before v's own turn in this tick, so v's
-          // scan peeks the queues the broadcast makes non-empty (sim.go:82-84).
-          const int pk = p.pick[v];
-          const int pj = (pk >> 6) == t ? (pk & 63) : 64;
-          for (int j = 0; j < od && j < pj; ++j)
-            if ((uint32_t)p.hq[ob + j] == kEmpty) ++c[1];
-        }
-        const unsigned long long draw0 = p.sc->base_trig + (unsigned long long)p.bsum[2 * (s0 / kGThreads)] +
-                                         (unsigned long long)p.ltrig[s0];
-        for (int j = 0; j < od; ++j) push_entry(p, ob + j, kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
-      }
-    }
-    int32_t j;
     const int32_t tok = p.tokens[v];
-    if (traffic_send(p, step, v, od, tok, &j)) {
-      // SendTokens(v, out-link j, 1): node.go:112-131
-      const unsigned long long draw = p.sc->base_send + (unsigned long long)p.bsum[2 * (v / kGThreads) + 1] +
-                                      (unsigned long long)p.lsend[v];
-      p.tokens[v] = tok - 1;
-      push_entry(p, ob + j, 1u, receive_time(p, draw, t), c[0]);
+    int32_t tj = -1;
+    const bool send = traffic_send(p, step, v, od, tok, &tj);
+    if (ncre && od <= kRegOd) {  // (a traffic send alone touches one channel: below)
+      if (od <= 8) push_node_reg<8>(p, t, v, ob, od, ncre, send, tok, tj, c);
+      else push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, c);
+    } else {
+      if (ncre) {
+        p.crn[v] = 0;
+        const int32_t lo = p.in_off[v];
+        uint64_t prev = 0;
+        for (int r = 0; r < ncre; ++r) {
+          const uint64_t best = next_creation(p, lo, ncre, r, prev);
+          prev = best;
+          const int32_t s0 = (int32_t)(best >> 32);
+          const uint32_t sid = (uint32_t)best;
+          if (r == 0 && s0 < v) {
+            // The reference delivers s0's marker before v's own turn in this tick, so v's
+            // scan peeks the queues the broadcast makes non-empty (sim.go:82-84).
+            const int pk = p.pick[v];
+            const int pj = (pk >> 6) == t ? (pk & 63) : 64;
+            for (int j = 0; j < od && j < pj; ++j)
+              if ((uint32_t)p.hq[ob + j] == kEmpty) ++c[1];
+          }
+          const unsigned long long draw0 = broadcast_draw(p, s0);
+          for (int j = 0; j < od; ++j) push_entry(p, ob + j, kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
+        }
+      }
+      if (send) {
+        // SendTokens(v, out-link j, 1): node.go:112-131
+        p.tokens[v] = tok - 1;
+        push_entry(p, ob + tj, 1u, receive_time(p, send_draw(p, v), t), c[0]);
+      }
     }
   }
   const int idx[2] = {GC_PUSH, GC_PEEK};
@@ -640,6 +749,7 @@ int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream) {
   hipError_t e;
   if ((e = hipMemsetAsync(p.W, 0xff, (size_t)p.s_cap * p.n * sizeof(uint64_t), s))) return e;
   if ((e = hipMemsetAsync(p.cnt, 0, (size_t)p.s_cap * p.n * sizeof(int32_t), s))) return e;
+  if ((e = hipMemsetAsync(p.done, 0, (size_t)p.s_cap * (1 + p.n_pblocks) * sizeof(int32_t), s))) return e;
   if ((e = hipMemsetAsync(p.sc, 0, sizeof(GScal), s))) return e;
   if ((e = hipMemsetAsync(p.cpart, 0, (size_t)kParts * kNumCnt * sizeof(unsigned long long), s))) return e;
   int64_t m = p.n > p.e ? p.n : p.e;
