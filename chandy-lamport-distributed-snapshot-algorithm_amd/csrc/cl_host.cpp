@@ -438,7 +438,7 @@ struct cl_sim {
     }
     Layout L = make_layout(n, od, id, cap_log2, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), s_cap,
                            row, kDelayStageWords);
-    if ((uint64_t)s_cap * stride * (uint64_t)std::max(n, std::max(C, 1)) >= (1ull << 32) ||
+    if (4ull * s_cap * stride * (uint64_t)std::max(n, std::max(C, 1)) >= (1ull << 32) ||  // byte offsets
         (uint64_t)L.state_words * stride >= (1ull << 32))
       return set_err(CL_E_LIMIT, "batch too large for 32-bit output indexing; split it");
     if ((int64_t)L.wave_words * kWavesPerBlock * 4 > kMaxLdsBytes)

@@ -65,7 +65,22 @@ struct Ctx {
   uint32_t inst;      // instance index (0 for lanes without an instance)
   uint32_t stride;    // padded instance count
   int32_t indeg, outdeg, out_off;
+  // snapshot outputs by 32-bit byte offsets from the (uniform) array bases: the stores use
+  // the SGPR-base + 32-bit-VGPR-offset form, with no 64-bit address arithmetic per store
+  uint32_t tok_lane, rec_lane, tick_lane;  // this lane's byte offset in sid plane 0
+  uint32_t tok_plane, rec_plane, tick_plane;  // bytes per sid plane (uniform)
+  bool mul24;  // every plane offset sid * plane fits the 24-bit multiplier
 };
+
+// Byte offset of snapshot plane `sid` (sid < 32).  v_mul_u32_u24 is a full-rate VALU op;
+// a generic 32-bit multiply is quarter rate, a 64-bit index computation several ops.
+__device__ __forceinline__ uint32_t plane_off(const Ctx& x, uint32_t sid, uint32_t plane) {
+  return x.mul24 ? __umul24(sid, plane) : sid * plane;
+}
+template <class T>
+__device__ __forceinline__ void st_at(T* base, uint32_t byte_off, T val) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off) = val;
+}
 
 struct Lane {
   int32_t tokens;
@@ -170,21 +185,20 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
                                              int32_t arrive) {
   const ExecParams& p = x.p;
   const Layout& lay = x.lay;
-  const uint32_t r = (uint32_t)sid * x.stride + x.inst;
-  p.snap_tok[r * p.n_nodes + x.v] = ln.tokens;
-  uint32_t* rec = p.snap_rec + r * p.n_ch;
+  st_at(p.snap_tok, plane_off(x, (uint32_t)sid, x.tok_plane) + x.tok_lane, ln.tokens);
+  const uint32_t rb = plane_off(x, (uint32_t)sid, x.rec_plane) + x.rec_lane;
   if constexpr (unrolled(D)) {
 #pragma unroll
     for (int32_t kj = 0; kj < D; ++kj) {
       if (kj < x.indeg) {
         const uint32_t cur = PW(lay.w_cur + kj);
-        rec[it[kj] >> 16] = kj == arrive ? (cur | (cur << 16)) : cur;
+        st_at(p.snap_rec, rb + ((it[kj] >> 16) << 2), kj == arrive ? (cur | (cur << 16)) : cur);
       }
     }
   } else {
     for (int32_t kj = 0; kj < x.indeg; ++kj) {
       const uint32_t cur = PW(lay.w_cur + kj);
-      rec[PW(lay.w_int + kj) >> 16] = kj == arrive ? (cur | (cur << 16)) : cur;
+      st_at(p.snap_rec, rb + ((PW(lay.w_int + kj) >> 16) << 2), kj == arrive ? (cur | (cur << 16)) : cur);
     }
   }
 }
@@ -194,7 +208,7 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
 __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
   const uint32_t old = lds_add(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
   if (old + 1 == (uint32_t)x.p.n_nodes) {
-    x.p.snap_tick[(uint32_t)sid * x.stride + x.inst] = ln.time;
+    st_at(x.p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + x.tick_lane, ln.time);
     lds_add(&XW(x.lay.x_ndone + x.seg), 1u);
   }
 }
@@ -239,9 +253,10 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
       ntrig++;
     }
   } else {  // later marker: stop recording this channel
-    const uint32_t r = (uint32_t)sid * x.stride + x.inst;
-    reinterpret_cast<uint16_t*>(x.p.snap_rec)[2 * (r * x.p.n_ch + (in_word<D>(x, it, ki) >> 16)) + 1] =
-        (uint16_t)PW(lay.w_cur + ki);
+    // hi16 of the cursor word: the channel's end
+    st_at(reinterpret_cast<uint16_t*>(x.p.snap_rec),
+          plane_off(x, (uint32_t)sid, x.rec_plane) + x.rec_lane + ((in_word<D>(x, it, ki) >> 16) << 2) + 2u,
+          (uint16_t)PW(lay.w_cur + ki));
     pend = ((pw >> sh) & 0xffu) - 1;
   }
   PW(pi) = (pw & ~(0xffu << sh)) | (pend << sh);
@@ -506,8 +521,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)first * p.sched_row);
     for (uint32_t k = lane; k < words; k += kWave) X[lay.x_delay + k] = src[k];
   }
+  const uint32_t C = (uint32_t)p.n_ch;
   const Ctx x{p, lay, X + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
-              indeg, outdeg, valid ? (int32_t)nb[2] : 0};
+              indeg, outdeg, valid ? (int32_t)nb[2] : 0,
+              4u * (ii * (uint32_t)N + (uint32_t)v), 4u * ii * C, 4u * ii,
+              4u * st * (uint32_t)N, 4u * st * C, 4u * st,
+              4ull * st * (uint64_t)max(N, (int32_t)C) < (1ull << 24)};
   InLinks<D> it;
   if constexpr (unrolled(D)) {
 #pragma unroll
