@@ -100,6 +100,8 @@ def lib():
         "cl_go_delay_schedule": [i64, i64, i64, vp],
         "cl_go_int63": [i64, i64, vp],
         "cl_go_intn": [i64, i32, i64, vp],
+        "cl_trace_enable": [vp, i64, i32, i32],
+        "cl_trace_read": [vp, i64, vp, i32, vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -108,6 +110,10 @@ def lib():
     L.cl_last_error.restype, L.cl_last_error.argtypes = cp, []
     _lib = L
     return L
+
+
+# Logger record kinds (include/clsnap.h CL_LOG_*)
+LOG_SENT_TOKEN, LOG_SENT_MARKER, LOG_RECV_TOKEN, LOG_RECV_MARKER, LOG_START, LOG_END = range(6)
 
 
 def _check(rc):
@@ -365,6 +371,45 @@ class ChandyLamportSim:
         out = np.zeros(len(SUM_NAMES), dtype=np.int64)
         _check(self._L.cl_get_checksums(self._h, _p(out)))
         return out
+
+    # ---- device event trace: the reference's debug Logger (logger.go:12-76) ------
+    def trace_enable(self, instance_lo=0, n_instances=1, capacity=4096):
+        """Record the Logger of instances [instance_lo, instance_lo + n_instances); the
+        next flush replays the event program with the trace build of the kernel."""
+        _check(self._L.cl_trace_enable(self._h, instance_lo, n_instances, capacity))
+
+    def trace(self, instance=0):
+        """LogEvents of one traced instance in Logger order: (epoch, kind, node rank,
+        other rank | -1, data, nodeTokens); kinds LOG_* (include/clsnap.h CL_LOG_*)."""
+        n = C.c_int32(0)
+        _check(self._L.cl_trace_read(self._h, instance, None, 0, C.byref(n)))
+        out = np.zeros((max(n.value, 1), 6), dtype=np.int32)
+        _check(self._L.cl_trace_read(self._h, instance, _p(out), n.value, C.byref(n)))
+        return [tuple(int(x) for x in r) for r in out[:n.value]]
+
+    def pretty_print(self, instance=0):
+        """Logger.PrettyPrint (logger.go:55-64) of a traced instance, as text."""
+        ids = self.node_ids()
+        name = lambda r: ids[r] if r >= 0 else "?"  # noqa: E731  (no link: the dest string is not kept)
+        lines, epoch = [], None
+        for ep, kind, node, other, data, tokens in self.trace(instance):
+            if ep != epoch:
+                lines.append(f"Time {ep}:")
+                epoch = ep
+            if kind == LOG_SENT_TOKEN:   # LogEvent.String / SentMsgRecord.String (logger.go:25-50, common.go:81-87)
+                rec, pre = f"{ids[node]} sent {data} tokens to {name(other)}", True
+            elif kind == LOG_SENT_MARKER:
+                rec, pre = f"{ids[node]} sent marker({data}) to {name(other)}", False
+            elif kind == LOG_RECV_TOKEN:  # ReceivedMsgRecord.String (common.go:116-122)
+                rec, pre = f"{ids[node]} received {data} tokens from {name(other)}", True
+            elif kind == LOG_RECV_MARKER:
+                rec, pre = f"{ids[node]} received marker({data}) from {name(other)}", False
+            elif kind == LOG_START:       # common.go:95-97
+                rec, pre = f"{ids[node]} startSnapshot({data})", True
+            else:                         # common.go:105-107
+                rec, pre = f"{ids[node]} endSnapshot({data})", False
+            lines.append(f"\t{ids[node]} has {tokens} token(s)\n\t{rec}" if pre else f"\t{rec}")
+        return "\n".join(lines) + ("\n" if lines else "")
 
     @staticmethod
     def status_string(code):

@@ -55,6 +55,28 @@ constexpr int32_t kWave = 64;
 constexpr int32_t kWavesPerBlock = 4;
 constexpr int32_t kMaxLdsBytes = 160 * 1024;
 
+// ---- device event trace (the reference's debug Logger, logger.go:12-76) -------
+// One 16-byte record per LogEvent.  Records of an instance are appended unordered and
+// sorted on the host by (epoch, order), which restates the Logger's sequence:
+//   epoch  = simulator time (Logger.NewEpoch per Tick, sim.go:73; test_common.go:35)
+//   order  = tick deliveries first, by delivering sender rank (sim.go:76-90): rank << 8 |
+//            sub, sub 0 = ReceivedMsgRecord (sim.go:86), 1 + j = SentMsgRecord of the
+//            broadcast on out-link j (node.go:100), 255 = EndSnapshotRecord (sim.go:127);
+//            then host events (bit 31) by device op index: op << 8 | sub, sub 0 =
+//            SentMsgRecord of SendTokens (node.go:118) or StartSnapshotRecord (sim.go:109),
+//            1 + j = the snapshot broadcast's SentMsgRecord on out-link j.
+enum TraceKind : uint32_t {
+  TK_SENT_TOKEN = 0, TK_SENT_MARKER = 1, TK_RECV_TOKEN = 2, TK_RECV_MARKER = 3,
+  TK_START = 4, TK_END = 5,
+};
+constexpr uint32_t kTraceNoLink = 127;  // SendTokens to a dest with no link (node.go:121-124)
+struct TraceRec {
+  uint32_t w0;     // epoch (bits 15..0) | kind (18..16) | node rank (24..19) | other rank (31..25)
+  uint32_t order;
+  int32_t data;    // Message.data: tokens or snapshot id
+  int32_t tokens;  // LogEvent.nodeTokens: the logged node's tokens at the event
+};
+
 // Pick word published by a sender lane each tick (phase A):
 //   bit 31 marker, bit 30 valid, bits 22..16 out-index, bits 15..0 payload.
 constexpr uint32_t kPickValid = 0x40000000u;
@@ -160,6 +182,12 @@ struct ExecParams {
   int32_t* snap_tick;  // [S_cap][stride]      completion tick or -1
   uint32_t* ovf;       // [C][1 << ocap_log2] spill ring
   uint32_t* ovh;       // [C] spill ring head
+  // event trace of instances [trace_lo, trace_lo + trace_n) (trace kernel build only)
+  TraceRec* trace;          // [trace_n][trace_cap]
+  uint32_t* trace_cnt;      // [trace_n] records emitted (may exceed trace_cap: overflow)
+  const int32_t* ch_dest;   // [C] dest rank of channel c
+  int64_t trace_lo;
+  int32_t trace_n, trace_cap;
 };
 
 struct SumParams {

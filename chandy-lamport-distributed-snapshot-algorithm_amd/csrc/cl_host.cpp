@@ -252,6 +252,12 @@ struct cl_sim {
   DevBuf<uint32_t> d_ovh;
   DevBuf<int32_t> d_hist;
   DevBuf<unsigned long long> d_sums;
+  // device event trace (cl_trace_enable): instances [trace_lo, trace_lo + trace_n)
+  DevBuf<TraceRec> d_trace;
+  DevBuf<uint32_t> d_trace_cnt;
+  DevBuf<int32_t> d_ch_dest;
+  int64_t trace_lo = 0;
+  int32_t trace_n = 0, trace_cap = 0;
 
   // host mirrors of results (invalidated by every launch)
   bool h_valid = false;
@@ -265,6 +271,7 @@ struct cl_sim {
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_tok.release(); d_snap_rec.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
       d_ovh.release(); d_hist.release(); d_sums.release();
+      d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       for (auto& e : ev_pool) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -379,6 +386,9 @@ struct cl_sim {
     int rc = d_topo.ensure(t.size());
     if (rc) return rc;
     HIP_TRY(hipMemcpy(d_topo.p, t.data(), t.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if ((rc = d_ch_dest.ensure(std::max<size_t>(ch_dst.size(), 1)))) return rc;
+    if (!ch_dst.empty())
+      HIP_TRY(hipMemcpy(d_ch_dest.p, ch_dst.data(), ch_dst.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     return CL_OK;
   }
 
@@ -526,6 +536,14 @@ struct cl_sim {
     p.snap_tick = d_snap_tick.p;
     p.ovf = d_ovf.p;
     p.ovh = d_ovh.p;
+    p.ch_dest = d_ch_dest.p;
+    if (trace_n > 0) {
+      p.trace = d_trace.p;
+      p.trace_cnt = d_trace_cnt.p;
+      p.trace_lo = trace_lo;
+      p.trace_n = trace_n;
+      p.trace_cap = trace_cap;
+    }
     return p;
   }
 
@@ -553,6 +571,11 @@ struct cl_sim {
     }
     int32_t started_before = 0;
     for (int32_t i = 0; i < begin; ++i) started_before += ops[i].kind == OP_SNAP;
+    if (trace_n > 0) {
+      if ((rc = d_trace.ensure((size_t)trace_n * trace_cap)) || (rc = d_trace_cnt.ensure((size_t)trace_n))) return rc;
+      // a replay from the initial state restarts the log (a resumed launch appends)
+      if (begin == 0) HIP_TRY(hipMemsetAsync(d_trace_cnt.p, 0, (size_t)trace_n * sizeof(uint32_t), stream));
+    }
     if (begin == 0) {
       HIP_TRY(hipMemsetAsync(d_snap_tick.p, 0xff, d_snap_tick.n * sizeof(int32_t), stream));
       if (lay.ocap_log2 >= 0) HIP_TRY(hipMemsetAsync(d_ovh.p, 0, d_ovh.n * sizeof(uint32_t), stream));
@@ -1121,3 +1144,50 @@ int cl_go_intn(int64_t seed, int32_t bound, int64_t n, int32_t* out) {
 }
 
 }  // extern "C"
+
+// ---- device event trace (logger.go) ------------------------------------------------
+int cl_trace_enable(cl_sim* sim, int64_t inst_lo, int32_t n_inst, int32_t cap) {
+  SIM_CHECK(sim);
+  if (n_inst < 0 || inst_lo < 0 || (n_inst > 0 && (inst_lo + n_inst > sim->n_inst || cap <= 0)))
+    return set_err(CL_E_INVALID, "trace range outside the batch");
+  sim->trace_lo = inst_lo;
+  sim->trace_n = n_inst;
+  sim->trace_cap = n_inst > 0 ? cap : 0;
+  sim->need_fresh = true;  // the next flush replays the program with the trace build
+  return CL_OK;
+}
+
+int cl_trace_read(cl_sim* sim, int64_t inst, cl_log_event* out, int32_t cap, int32_t* n_events) {
+  SIM_CHECK(sim);
+  if (!n_events) return set_err(CL_E_INVALID, "null output");
+  if (sim->trace_n <= 0 || inst < sim->trace_lo || inst >= sim->trace_lo + sim->trace_n)
+    return set_err(CL_E_INVALID, "instance %lld is not traced", (long long)inst);
+  int rc = sim->flush();
+  if (rc) return rc;
+  const size_t k = (size_t)(inst - sim->trace_lo);
+  uint32_t cnt = 0;
+  HIP_TRY(hipMemcpy(&cnt, sim->d_trace_cnt.p + k, sizeof cnt, hipMemcpyDeviceToHost));
+  const uint32_t have = std::min<uint32_t>(cnt, (uint32_t)sim->trace_cap);
+  std::vector<TraceRec> r(have);
+  if (have)
+    HIP_TRY(hipMemcpy(r.data(), sim->d_trace.p + k * sim->trace_cap, have * sizeof(TraceRec), hipMemcpyDeviceToHost));
+  // Logger order: by epoch, then tick deliveries by sender rank, then host events
+  std::sort(r.begin(), r.end(), [](const TraceRec& a, const TraceRec& b) {
+    const uint64_t ka = ((uint64_t)(a.w0 & 0xffffu) << 32) | a.order, kb = ((uint64_t)(b.w0 & 0xffffu) << 32) | b.order;
+    return ka < kb;
+  });
+  *n_events = (int32_t)have;
+  for (uint32_t i = 0; i < have && (int32_t)i < cap && out; ++i) {
+    const uint32_t w = r[i].w0, kind = (w >> 16) & 7u, other = w >> 25;
+    out[i].epoch = (int32_t)(w & 0xffffu);
+    out[i].kind = (int32_t)kind;
+    out[i].node = (int32_t)((w >> 19) & 63u);
+    out[i].other = (kind == TK_START || kind == TK_END || other == kTraceNoLink) ? -1 : (int32_t)other;
+    out[i].data = r[i].data;
+    out[i].tokens = r[i].tokens;
+  }
+  if (cnt > (uint32_t)sim->trace_cap)
+    return set_err(CL_E_LIMIT, "trace of instance %lld overflowed: %u records, capacity %d", (long long)inst, cnt,
+                   sim->trace_cap);
+  return CL_OK;
+}

@@ -82,6 +82,26 @@ __device__ __forceinline__ void st_at(T* base, uint32_t byte_off, T val) {
   *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off) = val;
 }
 
+// Append one Logger record (trace build only) for a traced instance.
+template <bool TRACE>
+__device__ __forceinline__ void temit(const Ctx& x, uint32_t kind, uint32_t other, int32_t epoch, uint32_t order,
+                                      int32_t data, int32_t tokens) {
+  if constexpr (TRACE) {
+    const int64_t k = (int64_t)x.inst - x.p.trace_lo;
+    if (k >= 0 && k < x.p.trace_n) {
+      const uint32_t slot = atomicAdd(&x.p.trace_cnt[k], 1u);
+      if (slot < (uint32_t)x.p.trace_cap) {
+        TraceRec r;
+        r.w0 = ((uint32_t)epoch & 0xffffu) | (kind << 16) | ((uint32_t)x.v << 19) | (other << 25);
+        r.order = order;
+        r.data = data;
+        r.tokens = tokens;
+        x.p.trace[k * x.p.trace_cap + slot] = r;
+      }
+    }
+  }
+}
+
 struct Lane {
   int32_t tokens;
   uint32_t started;
@@ -236,7 +256,7 @@ __device__ __forceinline__ uint32_t in_word(const Ctx& x, const InLinks<D>& it, 
 }
 
 // HandleMarker (node.go:149-171) for snapshot `sid` arriving on in-link ki from `src`.
-template <int D>
+template <int D, bool TRACE>
 __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLinks<D>& it, int32_t ki,
                                               uint32_t src, int32_t sid, int32_t& ntrig) {
   const Layout& lay = x.lay;
@@ -247,6 +267,10 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
     ln.started |= 1u << sid;
     create_local<D>(x, ln, it, sid, ki);
     pend = (uint32_t)x.indeg - 1;
+    if constexpr (TRACE)  // SendToNeighbors' SentMsgRecords (node.go:100)
+      for (int32_t j = 0; j < x.outdeg; ++j)
+        temit<TRACE>(x, TK_SENT_MARKER, (uint32_t)x.p.ch_dest[x.out_off + j], ln.time, (src << 8) | (1u + j), sid,
+                     ln.tokens);
     if (x.outdeg) {
       XW(lay.x_tslot + x.seg_base + src) = (uint32_t)x.outdeg;
       PW(lay.w_trig + ntrig) = src | ((uint32_t)sid << 8);
@@ -260,7 +284,10 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
     pend = ((pw >> sh) & 0xffu) - 1;
   }
   PW(pi) = (pw & ~(0xffu << sh)) | (pend << sh);
-  if (pend == 0) node_complete(x, ln, sid);
+  if (pend == 0) {
+    node_complete(x, ln, sid);
+    temit<TRACE>(x, TK_END, 0u, ln.time, (src << 8) | 255u, sid, ln.tokens);  // sim.go:127
+  }
 }
 
 // Pop from a channel whose younger packets spilled: refill the freed LDS slot (the ring's
@@ -278,7 +305,7 @@ __device__ __forceinline__ void refill(const Ctx& x, int32_t ko, uint32_t slot) 
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
 // Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
 // it[] holds this node's in-link words.
-template <int D, bool STAGED>
+template <int D, bool STAGED, bool TRACE>
 __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
@@ -345,13 +372,15 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       const bool mk = m && (pk & kMarkerBit);
       const bool tok = m && !mk;
       const uint32_t pay = pk & 0xffffu;
+      if constexpr (TRACE)  // ReceivedMsgRecord (sim.go:86), the receiver's tokens before handling
+        if (m) temit<TRACE>(x, mk ? TK_RECV_MARKER : TK_RECV_TOKEN, src, ln.time, src << 8, (int32_t)pay, ln.tokens);
       // HandleToken: tokens += data; the channel's recording cursor advances
       ln.tokens += tok ? (int32_t)pay : 0;
       ln.pop_tok += tok ? 1u : 0u;
       ln.pop_mk += mk ? 1u : 0u;
       const uint32_t cur = PW(lay.w_cur + ki);
       PW(lay.w_cur + ki) = cur + (tok ? 1u : 0u);
-      if (mk) handle_marker<D>(x, ln, it, ki, src, (int32_t)pay, ntrig);
+      if (mk) handle_marker<D, TRACE>(x, ln, it, ki, src, (int32_t)pay, ntrig);
     }
   } else if (act) {
 #pragma unroll
@@ -362,6 +391,8 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
       if (!(pk & kPickValid) || ((pk >> 16) & 0x7fu) != ((w >> 8) & 0xffu)) continue;
       const uint32_t pay = pk & 0xffffu;
+      temit<TRACE>(x, (pk & kMarkerBit) ? TK_RECV_MARKER : TK_RECV_TOKEN, src, ln.time, src << 8, (int32_t)pay,
+                   ln.tokens);
       if (!(pk & kMarkerBit)) {  // HandleToken: tokens += data; the recording cursor advances
         ln.pop_tok++;
         ln.tokens += (int32_t)pay;
@@ -369,7 +400,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
         continue;
       }
       ln.pop_mk++;
-      handle_marker<D>(x, ln, it, ki, src, (int32_t)pay, ntrig);
+      handle_marker<D, TRACE>(x, ln, it, ki, src, (int32_t)pay, ntrig);
     }
   }
   // ---- C/D: broadcast draws in sender order, then push -------------------------
@@ -412,11 +443,15 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
 
 // SendTokens (node.go:112-131) of one send event: balance check, link lookup, push -- all
 // at the sender.  Must be reached by all lanes of the wave.
-template <int D, bool STAGED>
-__device__ __forceinline__ void send_one(const Ctx& x, Lane& ln, const Op& op) {
+template <int D, bool STAGED, bool TRACE>
+__device__ __forceinline__ void send_one(const Ctx& x, Lane& ln, const Op& op, int32_t opi) {
   const bool me = ln.alive && x.v == op.a;
   const bool insufficient = me && ln.tokens < op.c;
   const bool fatal = ((__ballot(insufficient) >> (x.seg_base + op.a)) & 1ull) != 0;
+  if constexpr (TRACE)  // SentMsgRecord (node.go:118): after the balance check, before the link check
+    if (me && !insufficient)
+      temit<TRACE>(x, TK_SENT_TOKEN, op.b >= 0 ? (uint32_t)x.p.ch_dest[x.out_off + op.b] : kTraceNoLink, ln.time,
+                   0x80000000u | ((uint32_t)opi << 8), op.c, ln.tokens);
   if (me && !insufficient && op.b >= 0) {
     ln.tokens -= op.c;
 #pragma unroll
@@ -442,8 +477,9 @@ __device__ __forceinline__ void send_one(const Ctx& x, Lane& ln, const Op& op) {
 // its own event at once, with draw index draw + its position in the group.  If any event
 // of the wave would fail, the events run one by one (send_one), which freezes an instance
 // exactly where the sequential program does.
-template <int D, bool STAGED>
-__device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __restrict__ ev, int32_t k) {
+template <int D, bool STAGED, bool TRACE>
+__device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __restrict__ ev, int32_t k,
+                                           int32_t opi0) {
   const Layout& lay = x.lay;
   int32_t pos = -1, oj = 0, on = 0;
   for (int32_t q = 0; q < k; ++q) {
@@ -464,10 +500,12 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
     }
   }
   if (__builtin_expect(__ballot(bad) != 0, 0)) {
-    for (int32_t q = 0; q < k; ++q) send_one<D, STAGED>(x, ln, ev[q]);
+    for (int32_t q = 0; q < k; ++q) send_one<D, STAGED, TRACE>(x, ln, ev[q], opi0 + q);
     return;
   }
   if (mine) {
+    temit<TRACE>(x, TK_SENT_TOKEN, (uint32_t)x.p.ch_dest[x.out_off + oj], ln.time,
+                 0x80000000u | ((uint32_t)(opi0 + pos) << 8), on, ln.tokens);
     ln.tokens -= on;
 #pragma unroll
     for (int32_t j = 0; j < D; ++j)
@@ -492,7 +530,7 @@ constexpr int waves_for(int D) {
   return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1) : D == 4 ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : 1;
 }
 
-template <int D, bool STAGED>
+template <int D, bool STAGED, bool TRACE>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
                                                                          const Op* __restrict__ ops,
                                                                          const uint8_t* __restrict__ sched) {
@@ -582,10 +620,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     const Op op = ops[i];
     const unsigned long long ot0 = PROF_T();
     if (op.kind == OP_SEND) {
-      send_one<D, STAGED>(x, ln, op);
+      send_one<D, STAGED, TRACE>(x, ln, op, i);
       PROF_ADD(ln, 0, ot0);
     } else if (op.kind == OP_SENDS) {
-      send_group<D, STAGED>(x, ln, ops + i + 1, op.a);
+      send_group<D, STAGED, TRACE>(x, ln, ops + i + 1, op.a, i + 1);
       i += op.a;
       PROF_ADD(ln, 0, ot0);
     } else if (op.kind == OP_SNAP) {
@@ -593,6 +631,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
       if (ln.alive && v == op.a) {
         ln.started |= 1u << op.b;
         create_local<D>(x, ln, it, op.b, -1);
+        if constexpr (TRACE) {  // StartSnapshotRecord (sim.go:109), then SendToNeighbors (node.go:100)
+          const uint32_t o = 0x80000000u | ((uint32_t)i << 8);
+          temit<TRACE>(x, TK_START, 0u, ln.time, o, op.b, ln.tokens);
+          for (int32_t j = 0; j < outdeg; ++j)
+            temit<TRACE>(x, TK_SENT_MARKER, (uint32_t)p.ch_dest[x.out_off + j], ln.time, o | (1u + j), op.b, ln.tokens);
+        }
         const uint32_t pi = lay.w_pend + (op.b >> 2), sh = (op.b & 3) * 8;
         PW(pi) = (PW(pi) & ~(0xffu << sh)) | ((uint32_t)indeg << sh);
 #pragma unroll
@@ -618,7 +662,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
         }
         const bool act = ln.alive && (waiting || rem > 0);
         if (!__ballot(act)) break;
-        tick<D, STAGED>(x, ln, it, act);
+        tick<D, STAGED, TRACE>(x, ln, it, act);
         rem -= (act && !waiting) ? 1 : 0;
       }
 #if CLSNAP_PROF
@@ -761,25 +805,27 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
 
 }  // namespace
 
-template <int D, bool STAGED>
+template <int D, bool STAGED, bool TRACE>
 int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
   const size_t lds = (size_t)p.lay.wave_words * kWavesPerBlock * sizeof(uint32_t);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
   const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
   const unsigned blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED>), dim3(blocks), dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, p,
+  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE>), dim3(blocks), dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, p,
                      topo, ops, sched);
   return (int)hipGetLastError();
 }
 
 template <int D>
 int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
-  return p.lay.x_delay > 0 ? launch_exec_ds<D, true>(p, topo, ops, sched, stream)
-                           : launch_exec_ds<D, false>(p, topo, ops, sched, stream);
+  // The trace build reads delays from HBM (one instantiation per D, debug runs only).
+  if (p.trace_n > 0) return launch_exec_ds<D, false, true>(p, topo, ops, sched, stream);
+  return p.lay.x_delay > 0 ? launch_exec_ds<D, true, false>(p, topo, ops, sched, stream)
+                           : launch_exec_ds<D, false, false>(p, topo, ops, sched, stream);
 }
 
 // The kernel is instantiated for degree bounds 1, 2, 4, ... CLSNAP_MAX_D.

@@ -169,6 +169,32 @@ int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out /* [CL_NUM_COUNTE
 /* Batch checksums computed on the GPU (see CL_SUM_*); all-reduce them across ranks. */
 int cl_get_checksums(cl_sim* sim, int64_t* out /* [CL_NUM_SUMS] */);
 
+/* ---- device event trace: the reference's debug Logger (logger.go:12-76) ---- */
+/* One LogEvent (logger.go:18-23) per record, in the Logger's order.  Node ranks refer
+ * to cl_node_id; `other` is the peer of a Sent/Received record (-1 for Start/End and
+ * for a SendTokens to a dest without a link, node.go:121-124); tokens = nodeTokens. */
+#define CL_LOG_SENT_TOKEN 0     /* SentMsgRecord, token (node.go:118) */
+#define CL_LOG_SENT_MARKER 1    /* SentMsgRecord, marker (node.go:100) */
+#define CL_LOG_RECV_TOKEN 2     /* ReceivedMsgRecord, token (sim.go:86) */
+#define CL_LOG_RECV_MARKER 3    /* ReceivedMsgRecord, marker (sim.go:86) */
+#define CL_LOG_START_SNAPSHOT 4 /* StartSnapshotRecord (sim.go:109) */
+#define CL_LOG_END_SNAPSHOT 5   /* EndSnapshotRecord (sim.go:127) */
+typedef struct {
+  int32_t epoch;  /* Logger.events index = simulator time (sim.go:73, test_common.go:35) */
+  int32_t kind;   /* CL_LOG_* */
+  int32_t node;   /* LogEvent.nodeId (rank) */
+  int32_t other;  /* dest of a Sent record, src of a Received record (rank), else -1 */
+  int32_t data;   /* Message.data / snapshot id */
+  int32_t tokens; /* LogEvent.nodeTokens */
+} cl_log_event;
+/* Record the Logger of instances [inst_lo, inst_lo + n_inst) with room for cap events
+ * each (n_inst = 0: off, the default).  The next flush replays the program with the
+ * trace build of the kernel. */
+int cl_trace_enable(cl_sim* sim, int64_t inst_lo, int32_t n_inst, int32_t cap);
+/* The Logger of one traced instance: *n_events records, the first min(cap, *n_events)
+ * copied to out.  CL_E_LIMIT if the instance emitted more than the enabled capacity. */
+int cl_trace_read(cl_sim* sim, int64_t inst, cl_log_event* out, int32_t cap, int32_t* n_events);
+
 /* ---- delay-stream utility (host only) ------------------------------------ */
 /* out[i*draws + k] = k-th rand.Intn(5) of rand.Seed(seed_base + i), i in [0, n). */
 int cl_go_delay_schedule(int64_t seed_base, int64_t n, int64_t draws, uint8_t* out);

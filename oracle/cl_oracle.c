@@ -183,6 +183,15 @@ typedef struct {
     int64_t push, peek, pop_tok, pop_mk, recorded, draws, completed;
 } orc_counters;
 
+/* logger.go:18-23 LogEvent, with node IDs as sort ranks: {epoch, kind, node, other,
+ * data, nodeTokens}; kinds as CL_LOG_* in include/clsnap.h */
+enum { LOG_SENT_TOKEN = 0, LOG_SENT_MARKER, LOG_RECV_TOKEN, LOG_RECV_MARKER, LOG_START, LOG_END };
+typedef struct {
+    int64_t epoch;
+    int32_t kind, node, other;
+    int64_t data, tokens;
+} orc_log_rec;
+
 typedef struct orc_sim {
     int64_t time;              /* sim.go:13 */
     int next_snapshot_id;      /* sim.go:14 */
@@ -205,6 +214,10 @@ typedef struct orc_sim {
     int64_t sched_len, sched_pos;
     orc_counters cnt;
     int64_t drain_ticks;
+    /* Logger (logger.go:12-76): epoch = time (NewEpoch per Tick, sim.go:73) */
+    int log_on;
+    orc_log_rec* log;
+    int64_t n_log, cap_log;
 } orc_sim;
 
 static void* xrealloc(void* p, size_t n) {
@@ -241,6 +254,7 @@ void orc_free(orc_sim* s) {
     for (int i = 0; i < s->n_links; i++) queue_free(&s->links[i].q);
     free(s->nodes); free(s->links); free(s->sorted);
     free(s->completed_count); free(s->collected); free(s->completion_tick);
+    free(s->log);
     free(s);
 }
 
@@ -425,6 +439,38 @@ static orc_local* local_snap(orc_node* n, int sid) {
 }
 
 /* node.go:58-84 CreateLocalSnapshot; src_in = index into in_links or -1 for "" */
+static int rank_of(const orc_sim* s, int node) {
+    for (int a = 0; a < s->n_nodes; a++)
+        if (s->sorted[a] == node) return a;
+    return -1;
+}
+
+/* Logger.RecordEvent (logger.go:71-76): node's tokens at the time of the event */
+static void log_event(orc_sim* s, int kind, int node, int other, int64_t data) {
+    if (!s->log_on) return;
+    if (s->n_log == s->cap_log) {
+        s->cap_log = s->cap_log ? 2 * s->cap_log : 256;
+        s->log = (orc_log_rec*)xrealloc(s->log, sizeof(orc_log_rec) * (size_t)s->cap_log);
+    }
+    orc_log_rec* r = &s->log[s->n_log++];
+    r->epoch = s->time;
+    r->kind = kind;
+    r->node = rank_of(s, node);
+    r->other = other >= 0 ? rank_of(s, other) : -1;
+    r->data = data;
+    r->tokens = s->nodes[node].tokens;
+}
+
+void orc_log_enable(orc_sim* s, int on) { s->log_on = on; }
+int64_t orc_log_count(const orc_sim* s) { return s->n_log; }
+void orc_log_get(const orc_sim* s, int64_t* out /* [n_log][6] */) {
+    for (int64_t i = 0; i < s->n_log; i++) {
+        const orc_log_rec* r = &s->log[i];
+        int64_t* o = out + 6 * i;
+        o[0] = r->epoch; o[1] = r->kind; o[2] = r->node; o[3] = r->other; o[4] = r->data; o[5] = r->tokens;
+    }
+}
+
 static void create_local(orc_sim* s, int node, int sid, int src_in) {
     orc_node* n = &s->nodes[node];
     (void)s;
@@ -452,6 +498,7 @@ static int send_to_neighbors(orc_sim* s, int node, orc_msg m) {
     orc_node* n = &s->nodes[node];
     for (int k = 0; k < n->n_out; k++) {
         orc_link* l = &s->links[n->out_links[k]];
+        log_event(s, m.is_marker ? LOG_SENT_MARKER : LOG_SENT_TOKEN, node, l->dest, m.data); /* node.go:100 */
         orc_event e;
         e.src = l->src; e.dest = l->dest; e.msg = m;
         int rc = get_receive_time(s, &e.receive_time);
@@ -470,7 +517,8 @@ static int node_start_snapshot(orc_sim* s, int node, int sid) {
 }
 
 /* sim.go:126-131 NotifyCompletedSnapshot */
-static void notify_completed(orc_sim* s, int sid) {
+static void notify_completed(orc_sim* s, int node, int sid) {
+    log_event(s, LOG_END, node, -1, sid); /* sim.go:127 */
     s->completed_count[sid]++;
     if (s->completed_count[sid] == s->n_nodes) {
         s->completion_tick[sid] = s->time;
@@ -504,7 +552,7 @@ static int handle_packet(orc_sim* s, int node, int src, orc_msg m) {
         orc_local* l = local_snap(n, sid);
         if (l->num_links_being_recorded == 0) {
             l->finalized = 1; /* finalizeSnapshot: flattening happens at collect time */
-            notify_completed(s, sid);
+            notify_completed(s, node, sid);
         }
     } else {
         n->tokens += m.data;
@@ -538,6 +586,8 @@ int orc_tick(orc_sim* s) {
                 if (e->receive_time <= s->time) {
                     orc_event ev = queue_pop(&l->q);
                     if (ev.msg.is_marker) s->cnt.pop_mk++; else s->cnt.pop_tok++;
+                    log_event(s, ev.msg.is_marker ? LOG_RECV_MARKER : LOG_RECV_TOKEN, ev.dest, ev.src,
+                              ev.msg.data); /* sim.go:86 */
                     int rc = handle_packet(s, ev.dest, ev.src, ev.msg);
                     if (rc) { s->status = rc; return rc; }
                     break;
@@ -552,10 +602,12 @@ int orc_tick(orc_sim* s) {
 static int send_tokens_idx(orc_sim* s, int a, int b, int64_t num) {
     orc_node* n = &s->nodes[a];
     if (n->tokens < num) { s->status = ORC_FATAL_INSUFFICIENT_TOKENS; return s->status; }
-    n->tokens -= num;
     orc_link* l = NULL;
     for (int k = 0; k < n->n_out && b >= 0; k++)
         if (s->links[n->out_links[k]].dest == b) l = &s->links[n->out_links[k]];
+    /* node.go:118: logged before the link check; the record's dest is -1 without a link */
+    log_event(s, LOG_SENT_TOKEN, a, l ? b : -1, num);
+    n->tokens -= num;
     if (!l) { s->status = ORC_FATAL_UNKNOWN_DEST; return s->status; }
     orc_event e;
     e.src = a; e.dest = b; e.msg.is_marker = 0; e.msg.data = num;
@@ -578,6 +630,7 @@ static int start_snapshot_idx(orc_sim* s, int a, int* out_sid) {
     int sid = s->next_snapshot_id++;
     ensure_sids(s, sid);
     if (out_sid) *out_sid = sid;
+    log_event(s, LOG_START, a, -1, sid); /* sim.go:109 */
     int rc = node_start_snapshot(s, a, sid);
     if (rc) s->status = rc;
     return rc;
@@ -591,6 +644,7 @@ int orc_start_snapshot(orc_sim* s, const char* node, int* out_sid) {
     int sid = s->next_snapshot_id++;
     ensure_sids(s, sid);
     if (out_sid) *out_sid = sid;
+    log_event(s, LOG_START, a, -1, sid); /* sim.go:109 */
     int rc = node_start_snapshot(s, a, sid);
     if (rc) s->status = rc;
     return rc;

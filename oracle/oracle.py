@@ -70,6 +70,9 @@ def lib():
             "orc_collect_channels": (i64, [vp, C.c_int, vp, vp, vp, i64]),
             "orc_num_links": (C.c_int, [vp]),
             "orc_queue_depths": (None, [vp, vp]),
+            "orc_log_enable": (None, [vp, C.c_int]),
+            "orc_log_count": (i64, [vp]),
+            "orc_log_get": (None, [vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -192,6 +195,19 @@ class OracleSim:
 
     def snapshot_hash(self, sid):
         return self._L.orc_snapshot_hash(self._h, sid)
+
+    # ---- Logger (logger.go:12-76) ----------------------------------------------
+    def log_enable(self, on=True):
+        self._L.orc_log_enable(self._h, 1 if on else 0)
+
+    def log(self):
+        """LogEvents in Logger order: (epoch, kind, node rank, other rank | -1, data,
+        nodeTokens), kinds as CL_LOG_* (include/clsnap.h)."""
+        n = self._L.orc_log_count(self._h)
+        out = np.zeros((max(n, 1), 6), dtype=np.int64)
+        if n:
+            self._L.orc_log_get(self._h, _ptr(out))
+        return [tuple(int(x) for x in r) for r in out[:n]]
 
     # ---- synthetic large-graph workloads (DESIGN.md §10) ----------------------
     def use_counter_hash(self, seed):

@@ -14,7 +14,7 @@ import pytest
 
 import oracle as O
 from snapcheck import (ROOT, TEST_DATA, assert_equal, check_tokens, read_snapshot_file,
-                       scenarios)
+                       read_text, scenarios)
 
 KAT = json.load(open(os.path.join(ROOT, "tests", "golden", "go_rng_kat.json")))
 
@@ -104,3 +104,38 @@ def test_fatal_unknown_dest_and_hang():
     for _ in range(50):
         sim2.tick()
     assert not sim2.complete(0)
+
+
+def test_logger_restatement_simple_run():
+    """The oracle's Logger (logger.go:12-76) on 2nodes-simple at the golden seed, derived
+    by hand from the reference source: StartSnapshotRecord + the broadcast at time 0
+    (sim.go:109, node.go:100), N1's first marker at time 4 (sim.go:86, node.go:100,
+    sim.go:127: N1 has one in-link, so it completes at once), N2's closing marker at 7."""
+    ref = O.OracleSim()
+    ref.seed_go(O.REFERENCE_SEED)
+    assert ref.read_topology_text(read_text("2nodes.top")) == 0
+    ref.log_enable()
+    ref.read_events_text(read_text("2nodes-simple.events"))
+    # (epoch, kind, node rank, other rank, data, nodeTokens); ranks: N1 = 0, N2 = 1
+    assert ref.log() == [(0, 4, 1, -1, 0, 0), (0, 1, 1, 0, 0, 0),
+                         (4, 3, 0, 1, 0, 1), (4, 1, 0, 1, 0, 1), (4, 5, 0, -1, 0, 1),
+                         (7, 3, 1, 0, 0, 0), (7, 5, 1, -1, 0, 0)]
+
+
+@pytest.mark.parametrize("sc", scenarios(), ids=lambda s: s["name"])
+def test_logger_counts_match_counters(sc):
+    """Every scenario: one Received record per delivery, one Sent record per push, one
+    StartSnapshotRecord per snapshot, N EndSnapshotRecords per completed snapshot."""
+    ref = O.OracleSim()
+    ref.seed_go(O.REFERENCE_SEED)
+    assert ref.read_topology_text(read_text(sc["top"])) == 0
+    ref.log_enable()
+    ref.read_events_text(read_text(sc["events"]))
+    log, c = ref.log(), ref.counters()
+    kinds = [r[1] for r in log]
+    assert kinds.count(2) + kinds.count(3) == c["pop_tok"] + c["pop_mk"]
+    assert kinds.count(0) + kinds.count(1) == c["push"]
+    assert kinds.count(4) == ref.num_snapshots
+    n = len(ref.node_ids())
+    assert kinds.count(5) >= n * c["completed"]
+    assert [r[0] for r in log] == sorted(r[0] for r in log)  # epochs never go back
