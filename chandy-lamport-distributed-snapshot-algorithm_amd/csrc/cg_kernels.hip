@@ -476,7 +476,7 @@ __device__ inline void push_q(const GParams& p, int32_t c, uint64_t& q, uint32_t
 // k_push for a node of out-degree <= kRegOd with local snapshots created this tick: the node's head words are loaded once as
 // independent loads, every push of the tick (broadcasts in creating-sender order, then
 // the traffic send) updates them in registers, and they are stored once.
-constexpr int kRegOd = 16;
+constexpr int kRegOd = 8;
 template <int R>
 __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int32_t ob, int32_t od, int ncre,
                                      bool send, int32_t tok, int32_t tj, unsigned long long (&c)[2]) {
@@ -535,8 +535,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_
     int32_t tj = -1;
     const bool send = traffic_send(p, step, v, od, tok, &tj);
     if (ncre && od <= kRegOd) {  // (a traffic send alone touches one channel: below)
-      if (od <= 8) push_node_reg<8>(p, t, v, ob, od, ncre, send, tok, tj, c);
-      else push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, c);
+      push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, c);
     } else {
       if (ncre) {
         p.crn[v] = 0;
