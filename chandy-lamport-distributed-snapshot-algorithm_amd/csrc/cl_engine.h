@@ -118,6 +118,7 @@ struct Layout {
   int32_t x_delay;        // wave's delay rows staged in LDS (0 = not staged; rows read from HBM)
   int32_t shared;
   int32_t wave_words;
+  int32_t wpb;  // waves per workgroup: kWavesPerBlock, fewer when that many waves' state exceeds LDS
   // state image per instance (words): per node priv + G_NUM, then s_cap done counters + ndone
   int32_t state_words;
 };
@@ -132,6 +133,7 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
   L.s_cap = s_cap;
   L.sp = (s_cap + 3) / 4;
   L.ipw = n_nodes > 0 ? kWave / n_nodes : 0;
+  L.wpb = kWavesPerBlock;
   L.w_fifo = 0;
   L.w_chw = od << cap_log2;
   L.w_cur = L.w_chw + od;

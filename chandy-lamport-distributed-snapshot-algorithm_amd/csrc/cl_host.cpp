@@ -451,7 +451,9 @@ struct cl_sim {
     if (4ull * s_cap * stride * (uint64_t)std::max(n, std::max(C, 1)) >= (1ull << 32) ||  // byte offsets
         (uint64_t)L.state_words * stride >= (1ull << 32))
       return set_err(CL_E_LIMIT, "batch too large for 32-bit output indexing; split it");
-    if ((int64_t)L.wave_words * kWavesPerBlock * 4 > kMaxLdsBytes)
+    // high-degree topologies: fewer waves per workgroup (one wave's state must fit)
+    while (L.wpb > 1 && (int64_t)L.wave_words * L.wpb * 4 > kMaxLdsBytes) L.wpb /= 2;
+    if ((int64_t)L.wave_words * L.wpb * 4 > kMaxLdsBytes)
       return set_err(CL_E_LIMIT, "per-wave state of %d words exceeds LDS (lower fifo slots or degree)", L.wave_words);
     lay = L;
     layout_row = row;

@@ -539,7 +539,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   const int32_t N = p.n_nodes;
   const int32_t lane = threadIdx.x & (kWave - 1);
   const int32_t wib = threadIdx.x / kWave;
-  const uint32_t wave = blockIdx.x * kWavesPerBlock + wib;
+  const uint32_t wave = blockIdx.x * (uint32_t)p.lay.wpb + wib;
   lds_u32* X = (lds_u32*)(lds + (size_t)wib * lay.wave_words);
   const int32_t seg = lane / N;
   const int32_t v = lane - seg * N;
@@ -807,15 +807,16 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
 
 template <int D, bool STAGED, bool TRACE>
 int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
-  const size_t lds = (size_t)p.lay.wave_words * kWavesPerBlock * sizeof(uint32_t);
+  const int32_t wpb = p.lay.wpb;
+  const size_t lds = (size_t)p.lay.wave_words * wpb * sizeof(uint32_t);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
   const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
-  const unsigned blocks = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE>), dim3(blocks), dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, p,
+  const unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
+  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE>), dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)stream, p,
                      topo, ops, sched);
   return (int)hipGetLastError();
 }
