@@ -279,7 +279,7 @@ def bench_graph(args, rank, world, local_rank):
                        "final_residual": tot["final_residual"], "digest": tot["digest"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "graph tick pipeline (k_pick, k_marker, k_expand, k_tally, k_scan, k_push)",
+                         "kernel": "graph tick pipeline (k_hostops, k_pick, k_marker, k_scan, k_push)",
                          "kernel_ms": avg_run_ms, "alg_bytes_per_launch": alg},
             "cpu_baseline": cpu,
         }

@@ -1,0 +1,12 @@
+# HBM traffic of the graph engine (configs c4/c5): FETCH_SIZE and WRITE_SIZE passes, each in
+# its own rocprofv3 run (MI355X_MICROARCH.md HBM section), over one flush + one timed run.
+# usage: CFG=c4|c5 bash tools/gpu_pmc_graph.sh   -> gpurun_out/pmcg_<cfg>/pass{3,4}/
+set -e
+CFG=${CFG:-c4}
+OUT=$GRAFT_REPO_ROOT/gpurun_out/pmcg_$CFG
+rm -rf $OUT; mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp
+P=$GRAFT_REPO_ROOT/bench.py
+ARGS="--config $CFG --steps 1 --warmup 0 --no-cpu-baseline"
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pass3 -o p -- python3 $P $ARGS > $OUT/pass3.log 2>&1
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pass4 -o p -- python3 $P $ARGS > $OUT/pass4.log 2>&1
