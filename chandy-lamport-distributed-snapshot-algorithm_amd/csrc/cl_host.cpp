@@ -578,10 +578,8 @@ struct cl_sim {
       // a replay from the initial state restarts the log (a resumed launch appends)
       if (begin == 0) HIP_TRY(hipMemsetAsync(d_trace_cnt.p, 0, (size_t)trace_n * sizeof(uint32_t), stream));
     }
-    if (begin == 0) {
-      HIP_TRY(hipMemsetAsync(d_snap_tick.p, 0xff, d_snap_tick.n * sizeof(int32_t), stream));
-      if (lay.ocap_log2 >= 0) HIP_TRY(hipMemsetAsync(d_ovh.p, 0, d_ovh.n * sizeof(uint32_t), stream));
-    }
+    // (a fresh replay's kernel sets snap_tick to -1 itself: cl_exec_kernel prologue)
+    if (begin == 0 && lay.ocap_log2 >= 0) HIP_TRY(hipMemsetAsync(d_ovh.p, 0, d_ovh.n * sizeof(uint32_t), stream));
     ExecParams p = exec_params(begin, started_before);
     p.save_state = save_state ? 1 : 0;
     if (ev_used == 256 && (rc = fold_events())) return rc;

@@ -581,6 +581,12 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
 #endif
   for (int32_t k = lane; k < lay.x_delay_begin; k += kWave) XW(lay.priv * kWave + k) = 0u;
   if (p.fresh) {
+    // completion ticks start at -1 (no separate fill launch before every replay); the wait
+    // orders these stores before any completion store of the same wave
+    if (valid)
+      for (int32_t sid = v; sid < lay.s_cap; sid += N)
+        st_at(p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + x.tick_lane, (int32_t)-1);
+    __builtin_amdgcn_s_waitcnt(0);
     for (int32_t k = 0; k < lay.priv; ++k) PW(k) = 0u;
     ln.tokens = valid ? (int32_t)topo[(size_t)N * p.topo_w + v] : 0;
     ln.started = 0;
