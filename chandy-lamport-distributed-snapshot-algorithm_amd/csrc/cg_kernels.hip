@@ -240,9 +240,33 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
 __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
   if (block_frozen(p)) return;
   __shared__ int s_m;
-  if (threadIdx.x == 0) s_m = 0;
-  __syncthreads();
+  // Head receiveTime words of the block's senders: the block's out-channels are one
+  // contiguous CSR range, loaded once with coalesced loads (a lane-per-sender prefetch
+  // touched 64 separate 64 B segments per wave instruction).  Channels past kStage
+  // (blocks of unusually high out-degree) are read from HBM by their sender.
+  constexpr int kStage = kGThreads * 12;
+  __shared__ uint64_t s_hq[kStage];
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t blo = p.out_off[blockIdx.x * kGThreads];
+  const int32_t bhi = p.out_off[min((int)(blockIdx.x + 1) * kGThreads, p.n)];
+  const int32_t nst = min(bhi - blo, kStage);
+  if (threadIdx.x == 0) s_m = 0;
+  {
+    // all loads issued before the first LDS store: one HBM latency, not one per stride
+    constexpr int kPer = kStage / kGThreads;
+    uint64_t tmp[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int32_t i = threadIdx.x + k * kGThreads;
+      tmp[k] = i < nst ? p.hq[blo + i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int32_t i = threadIdx.x + k * kGThreads;
+      if (i < nst) s_hq[i] = tmp[k];
+    }
+  }
+  __syncthreads();
   if (s == 0) {
     p.sc->time = t;  // time++ (sim.go:72)
     p.sc->big_n = 0;
@@ -250,24 +274,12 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
   unsigned long long c[3] = {0, 0, 0};  // peek, pop_tok, pop_mk
   if (s < p.n) {
     const int32_t base = p.out_off[s], od = p.out_off[s + 1] - base;
-    // The first kPre head words are loaded up front as independent loads (one HBM
-    // latency instead of a chain of od); the scan below reads them from registers.
-    constexpr int kPre = 8;
-    uint32_t pre[kPre];
-#pragma unroll
-    for (int j = 0; j < kPre; ++j) pre[j] = j < od ? (uint32_t)p.hq[base + j] : kEmpty;
-    int first = -1;
-#pragma unroll
-    for (int j = 0; j < kPre; ++j) {
-      const bool live = first < 0 && pre[j] != kEmpty;
-      c[0] += live ? 1 : 0;  // Queue.Peek, sim.go:83
-      first = live && pre[j] <= (uint32_t)t ? j : first;
-    }
-    for (int j = first >= 0 ? first : kPre; j < od; ++j) {
-      const uint64_t q = p.hq[base + j];
+    for (int j = 0; j < od; ++j) {
+      const int32_t li = base + j - blo;
+      const uint64_t q = li < kStage ? s_hq[li] : p.hq[base + j];
       const uint32_t rt = (uint32_t)q;
       if (rt == kEmpty) continue;
-      if (j >= kPre) ++c[0];  // Queue.Peek, sim.go:83 (heads past the prefetch)
+      ++c[0];  // Queue.Peek, sim.go:83
       if (rt > (uint32_t)t) continue;
       const int32_t ch = base + j;
       const uint32_t hc = (uint32_t)(q >> 32), capm = (1u << p.cap_log2) - 1;
