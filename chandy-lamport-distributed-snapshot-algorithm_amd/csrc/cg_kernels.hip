@@ -485,19 +485,29 @@ __device__ inline void push_q(const GParams& p, int32_t c, uint64_t& q, uint32_t
   ++pushes;
 }
 
-// k_push for a node of out-degree <= kRegOd with local snapshots created this tick: the node's head words are loaded once as
-// independent loads, every push of the tick (broadcasts in creating-sender order, then
-// the traffic send) updates them in registers, and they are stored once.
+// k_push for a node with local snapshots created this tick, in chunks of R out-channels:
+// a chunk's head words are loaded once as independent loads, every push of the tick onto
+// the chunk (broadcasts in creating-sender order, then the traffic send) updates them in
+// registers, and they are stored once -- one HBM round trip per chunk instead of a chain
+// of one per channel for nodes of high out-degree.  Per channel the push order is the
+// reference's (queue.go:18-20); draw indices are the absolute out-link positions.
 constexpr int kRegOd = 8;
 template <int R>
 __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int32_t ob, int32_t od, int ncre,
                                      bool send, int32_t tok, int32_t tj, unsigned long long (&c)[2]) {
-  uint64_t q[R];
+  p.crn[v] = 0;
+  const int32_t lo = p.in_off[v];
+  uint32_t srt = 0;
+  if (send) {
+    // SendTokens(v, out-link tj, 1): node.go:112-131
+    p.tokens[v] = tok - 1;
+    srt = receive_time(p, send_draw(p, v), t);
+  }
+  for (int32_t j0 = 0; j0 < od; j0 += R) {
+    const int32_t m = od - j0 < R ? od - j0 : R, obc = ob + j0;
+    uint64_t q[R];
 #pragma unroll
-  for (int j = 0; j < R; ++j) q[j] = j < od ? p.hq[ob + j] : 0ull;
-  if (ncre) {
-    p.crn[v] = 0;
-    const int32_t lo = p.in_off[v];
+    for (int j = 0; j < R; ++j) q[j] = j < m ? p.hq[obc + j] : 0ull;
     uint64_t prev = 0;
     for (int r = 0; r < ncre; ++r) {
       const uint64_t best = next_creation(p, lo, ncre, r, prev);
@@ -511,25 +521,22 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
         const int pj = (pk >> 6) == t ? (pk & 63) : 64;
 #pragma unroll
         for (int j = 0; j < R; ++j)
-          if (j < od && j < pj && (uint32_t)q[j] == kEmpty) ++c[1];
+          if (j < m && j0 + j < pj && (uint32_t)q[j] == kEmpty) ++c[1];
       }
-      const unsigned long long draw0 = broadcast_draw(p, s0);
+      const unsigned long long draw0 = broadcast_draw(p, s0) + (unsigned long long)j0;
 #pragma unroll
       for (int j = 0; j < R; ++j)
-        if (j < od) push_q(p, ob + j, q[j], kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
+        if (j < m) push_q(p, obc + j, q[j], kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
     }
-  }
-  if (send) {
-    // SendTokens(v, out-link tj, 1): node.go:112-131
-    p.tokens[v] = tok - 1;
-    const uint32_t rt = receive_time(p, send_draw(p, v), t);
+    if (send) {
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-      if (j == tj) push_q(p, ob + j, q[j], 1u, rt, c[0]);
-  }
+      for (int j = 0; j < R; ++j)
+        if (j0 + j == tj) push_q(p, obc + j, q[j], 1u, srt, c[0]);
+    }
 #pragma unroll
-  for (int j = 0; j < R; ++j) {
-    if (j < od && (ncre || j == tj)) p.hq[ob + j] = q[j];
+    for (int j = 0; j < R; ++j) {
+      if (j < m) p.hq[obc + j] = q[j];
+    }
   }
 }
 
@@ -546,35 +553,12 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_
     const int32_t tok = p.tokens[v];
     int32_t tj = -1;
     const bool send = traffic_send(p, step, v, od, tok, &tj);
-    if (ncre && od <= kRegOd) {  // (a traffic send alone touches one channel: below)
+    if (ncre) {
       push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, c);
-    } else {
-      if (ncre) {
-        p.crn[v] = 0;
-        const int32_t lo = p.in_off[v];
-        uint64_t prev = 0;
-        for (int r = 0; r < ncre; ++r) {
-          const uint64_t best = next_creation(p, lo, ncre, r, prev);
-          prev = best;
-          const int32_t s0 = (int32_t)(best >> 32);
-          const uint32_t sid = (uint32_t)best;
-          if (r == 0 && s0 < v) {
-            // The reference delivers s0's marker before v's own turn in this tick, so v's
-            // scan peeks the queues the broadcast makes non-empty (sim.go:82-84).
-            const int pk = p.pick[v];
-            const int pj = (pk >> 6) == t ? (pk & 63) : 64;
-            for (int j = 0; j < od && j < pj; ++j)
-              if ((uint32_t)p.hq[ob + j] == kEmpty) ++c[1];
-          }
-          const unsigned long long draw0 = broadcast_draw(p, s0);
-          for (int j = 0; j < od; ++j) push_entry(p, ob + j, kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
-        }
-      }
-      if (send) {
-        // SendTokens(v, out-link j, 1): node.go:112-131
-        p.tokens[v] = tok - 1;
-        push_entry(p, ob + tj, 1u, receive_time(p, send_draw(p, v), t), c[0]);
-      }
+    } else if (send) {
+      // SendTokens(v, out-link j, 1): node.go:112-131 (one channel: no batching)
+      p.tokens[v] = tok - 1;
+      push_entry(p, ob + tj, 1u, receive_time(p, send_draw(p, v), t), c[0]);
     }
   }
   const int idx[2] = {GC_PUSH, GC_PEEK};
