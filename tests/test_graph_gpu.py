@@ -81,6 +81,40 @@ def _random_graph(rng, n):
     return rng.integers(0, n, m).astype(np.int32), rng.integers(0, n, m).astype(np.int32)
 
 
+def _random_events_run(rng, n, src, dst, gseed, n_events, drain=500, tokens=(0, 50),
+                       link_sends=False):
+    ids = [f"n{r}" for r in rng.permutation(n)]
+    top = f"{n}\n" + "".join(f"{ids[r]} {int(rng.integers(*tokens))}\n" for r in range(n)) + \
+        "".join(f"{ids[a]} {ids[b]}\n" for a, b in zip(src, dst))
+    ev = []
+    for _ in range(n_events):
+        x = rng.random()
+        if x < 0.45:
+            a, b = int(rng.integers(0, n)), int(rng.integers(0, n))
+            if link_sends:  # an existing channel: no unknown-dest fatal
+                e = int(rng.integers(0, len(src)))
+                a, b = int(src[e]), int(dst[e])
+            ev.append(f"send {ids[a]} {ids[b]} {int(rng.integers(0, 8))}")
+        elif x < 0.6:
+            ev.append(f"snapshot {ids[int(rng.integers(0, n))]}")
+        else:
+            ev.append(f"tick {int(rng.integers(1, 4))}")
+    events = "\n".join(ev) + "\n"
+    o = O.OracleSim()
+    o.seed_go(gseed)
+    assert o.read_topology_text(top) == 0
+    o.read_events_text(events, drain)
+    if os.environ.get("CG_ORACLE_ONLY"):  # sizing aid on a CPU host
+        return o
+    g = clg.GraphSim(max_drain_ticks=drain)
+    g.read_topology_text(top)
+    g.set_delay_go_seed(gseed)
+    g.read_events_text(events)
+    g.flush()
+    compare(g, o)
+    return o
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_random_host_events_vs_oracle(seed):
     """Random digraphs with host sends of arbitrary sizes (payload history), snapshots
@@ -89,31 +123,19 @@ def test_random_host_events_vs_oracle(seed):
     rng = np.random.default_rng(seed)
     n = int(rng.integers(2, 30))
     src, dst = _random_graph(rng, n)
-    ids = [f"n{r}" for r in rng.permutation(n)]
-    top = f"{n}\n" + "".join(f"{ids[r]} {int(rng.integers(0, 50))}\n" for r in range(n)) + \
-        "".join(f"{ids[a]} {ids[b]}\n" for a, b in zip(src, dst))
-    ev = []
-    for _ in range(int(rng.integers(5, 40))):
-        x = rng.random()
-        if x < 0.45:
-            a, b = int(rng.integers(0, n)), int(rng.integers(0, n))
-            ev.append(f"send {ids[a]} {ids[b]} {int(rng.integers(0, 8))}")
-        elif x < 0.6:
-            ev.append(f"snapshot {ids[int(rng.integers(0, n))]}")
-        else:
-            ev.append(f"tick {int(rng.integers(1, 4))}")
-    events = "\n".join(ev) + "\n"
-    gseed = O.REFERENCE_SEED + seed
-    g = clg.GraphSim(max_drain_ticks=500)
-    g.read_topology_text(top)
-    g.set_delay_go_seed(gseed)
-    g.read_events_text(events)
-    g.flush()
-    o = O.OracleSim()
-    o.seed_go(gseed)
-    assert o.read_topology_text(top) == 0
-    o.read_events_text(events, 500)
-    compare(g, o)
+    _random_events_run(rng, n, src, dst, O.REFERENCE_SEED + seed, int(rng.integers(5, 40)))
+
+
+@pytest.mark.parametrize("n,deg,seed", [(24, 23, 0), (70, 40, 1), (100, 62, 2)])
+def test_high_out_degree_vs_oracle(n, deg, seed):
+    """Dense digraphs: broadcasts over out-degrees up to 62 (k_push pushes them in chunks
+    of 8 channels), and one pick block whose out-channels exceed k_pick's LDS stage
+    (3,072 head words; n=70/100 have 2,800 / 6,200), so the fallback reads HBM."""
+    rng = np.random.default_rng(100 + seed)
+    src = np.repeat(np.arange(n), deg)
+    dst = np.concatenate([rng.choice(np.delete(np.arange(n), v), deg, replace=False) for v in range(n)])
+    _random_events_run(rng, n, src.astype(np.int32), dst.astype(np.int32), O.REFERENCE_SEED + 77 + seed, 60,
+                       drain=4000, tokens=(100, 200), link_sends=True)
 
 
 def test_rerun_and_incremental_equal_one_shot():
