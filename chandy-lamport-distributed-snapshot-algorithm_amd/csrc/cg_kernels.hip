@@ -175,14 +175,18 @@ __device__ inline void block_exclusive_scan2(long long& a, long long& b, long lo
 
 // Block tally of node rank v = blockIdx.x * kGThreads + threadIdx.x: `trig` draws
 // triggered by v's delivery this tick, and v's traffic send of step `step`.
-__device__ inline void tally(const GParams& p, int32_t trig, int32_t step) {
+// The node's traffic-send bit for the tally (loads issued by the caller at kernel start,
+// ahead of the block's first barrier).
+__device__ inline int32_t tally_send_bit(const GParams& p, int32_t step) {
+  const int v = blockIdx.x * kGThreads + threadIdx.x;
+  int32_t j;
+  return v < p.n && traffic_send(p, step, v, p.out_off[v + 1] - p.out_off[v], p.tokens[v], &j) ? 1 : 0;
+}
+
+__device__ inline void tally(const GParams& p, int32_t trig, int32_t sendbit) {
   __shared__ long long sh[2 * (kGThreads / 64)];
   const int v = blockIdx.x * kGThreads + threadIdx.x;
-  long long a = trig, b = 0;
-  if (v < p.n) {
-    int32_t j;
-    b = traffic_send(p, step, v, p.out_off[v + 1] - p.out_off[v], p.tokens[v], &j) ? 1 : 0;
-  }
+  long long a = trig, b = sendbit;
   const long long a0 = a, b0 = b;
   long long ta, tb;
   block_exclusive_scan2(a, b, ta, tb, sh);
@@ -238,7 +242,6 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
 // tick phase A: pick + deliver
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
-  if (block_frozen(p)) return;
   __shared__ int s_m;
   // Head receiveTime words of the block's senders: the block's out-channels are one
   // contiguous CSR range, loaded once with coalesced loads (a lane-per-sender prefetch
@@ -250,6 +253,13 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
   const int32_t blo = p.out_off[blockIdx.x * kGThreads];
   const int32_t bhi = p.out_off[min((int)(blockIdx.x + 1) * kGThreads, p.n)];
   const int32_t nst = min(bhi - blo, kStage);
+  int32_t base = 0, od = 0;
+  if (s < p.n) {
+    base = p.out_off[s];
+    od = p.out_off[s + 1] - base;
+  }
+  // (topology loads above are in flight during the status check: one latency, not two)
+  if (block_frozen(p)) return;
   if (threadIdx.x == 0) s_m = 0;
   {
     // all loads issued before the first LDS store: one HBM latency, not one per stride
@@ -273,7 +283,6 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
   }
   unsigned long long c[3] = {0, 0, 0};  // peek, pop_tok, pop_mk
   if (s < p.n) {
-    const int32_t base = p.out_off[s], od = p.out_off[s + 1] - base;
     for (int j = 0; j < od; ++j) {
       const int32_t li = base + j - blo;
       const uint64_t q = li < kStage ? s_hq[li] : p.hq[base + j];
@@ -321,6 +330,10 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
 // tick phase B: the markers delivered by pick block b's senders, and block b's tally
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t t) {
+  // the tally's inputs (node tokens after this tick's deliveries, out-degree) and the
+  // block's marker count are loaded while the status check is in flight
+  const int32_t sendbit = tally_send_bit(p, t);
+  const int nm = p.mcnt[blockIdx.x];
   if (block_frozen(p)) return;
   __shared__ int s_nb, s_base;
   __shared__ int s_trig[kGThreads];
@@ -335,7 +348,6 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t t) {
   s_ctsum[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_nb = 0;
   __syncthreads();
-  const int nm = p.mcnt[blockIdx.x];
   unsigned long long c[2] = {0, 0};  // recorded, completed
   bool done = false;
   int32_t sid = 0, vdone = 0;
@@ -402,14 +414,15 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t t) {
   __syncthreads();
   if (cslot >= 0) p.stok[(size_t)bx.sid * p.n + bx.v] = p.tokens[bx.v] - s_ctsum[cslot];
   if (threadIdx.x == 0 && s_nb) s_base = atomicAdd(&p.sc->big_n, s_nb);
-  tally(p, s_trig[threadIdx.x], t);  // (has a barrier: s_base is final below)
+  tally(p, s_trig[threadIdx.x], sendbit);  // (has a barrier: s_base is final below)
   if (bslot >= 0) p.big[s_base + bslot] = bx;
 }
 
 // Step-0 traffic tally (before the first tick: no triggers).
 __global__ void __launch_bounds__(kGThreads) k_tally(GParams p, int32_t step) {
+  const int32_t sendbit = tally_send_bit(p, step);
   if (block_frozen(p)) return;
-  tally(p, 0, step);
+  tally(p, 0, sendbit);
 }
 
 // phase C: exclusive scan of the block tallies (one workgroup, 4 entries per thread),
@@ -544,13 +557,17 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
 // snapshots created at it this tick (in creating-sender order), then its traffic send;
 // then the grid expands the local snapshots created at high in-degree nodes.
 __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_t step) {
-  if (block_frozen(p)) return;
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  int32_t ob = 0, od = 0, ncre = 0, tok = 0;
+  if (v < p.n) {  // loaded while the status check is in flight
+    ob = p.out_off[v];
+    od = p.out_off[v + 1] - ob;
+    ncre = p.crn[v];
+    tok = p.tokens[v];
+  }
+  if (block_frozen(p)) return;
   unsigned long long c[2] = {0, 0};  // push, peek
   if (v < p.n) {
-    const int32_t ob = p.out_off[v], od = p.out_off[v + 1] - ob;
-    const int ncre = p.crn[v];
-    const int32_t tok = p.tokens[v];
     int32_t tj = -1;
     const bool send = traffic_send(p, step, v, od, tok, &tj);
     if (ncre) {
