@@ -555,8 +555,8 @@ struct cl_graph {
     if (!fresh && executed == prog.size()) return CL_OK;
     if (ev_used == ev_pool.size()) {
       std::pair<hipEvent_t, hipEvent_t> pr;
-      GHIP(hipEventCreate(&pr.first));
-      GHIP(hipEventCreate(&pr.second));
+      GHIP(hipEventCreateWithFlags(&pr.first, hipEventDisableSystemFence));  // timing only: no cache writeback per record
+      GHIP(hipEventCreateWithFlags(&pr.second, hipEventDisableSystemFence));
       ev_pool.push_back(pr);
     }
     auto& ev = ev_pool[ev_used++];
