@@ -578,8 +578,8 @@ struct cl_sim {
       // a replay from the initial state restarts the log (a resumed launch appends)
       if (begin == 0) HIP_TRY(hipMemsetAsync(d_trace_cnt.p, 0, (size_t)trace_n * sizeof(uint32_t), stream));
     }
-    // (a fresh replay's kernel sets snap_tick to -1 itself: cl_exec_kernel prologue)
-    if (begin == 0 && lay.ocap_log2 >= 0) HIP_TRY(hipMemsetAsync(d_ovh.p, 0, d_ovh.n * sizeof(uint32_t), stream));
+    // (a fresh replay's kernel sets snap_tick to -1 and the spill ring heads to 0 itself:
+    // cl_exec_kernel prologue -- no fill launch before every replay)
     ExecParams p = exec_params(begin, started_before);
     p.save_state = save_state ? 1 : 0;
     if (ev_used == 256 && (rc = fold_events())) return rc;

@@ -586,6 +586,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     if (valid)
       for (int32_t sid = v; sid < lay.s_cap; sid += N)
         st_at(p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + x.tick_lane, (int32_t)-1);
+    // HBM spill ring heads start at 0 likewise: every lane owns its out-channels' heads
+    // (only their sender pushes, refills and counts them)
+    if (valid && lay.ocap_log2 >= 0)
+      for (int32_t ko = 0; ko < outdeg; ++ko) p.ovh[(uint32_t)(x.out_off + ko) * st + ii] = 0u;
     __builtin_amdgcn_s_waitcnt(0);
     for (int32_t k = 0; k < lay.priv; ++k) PW(k) = 0u;
     ln.tokens = valid ? (int32_t)topo[(size_t)N * p.topo_w + v] : 0;
