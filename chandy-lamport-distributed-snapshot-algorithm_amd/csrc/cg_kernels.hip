@@ -628,10 +628,12 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, int32_t ob, int32_t oc) {
   __shared__ int s_stop;
+  __shared__ unsigned long long s_draw;
   unsigned long long pushes = 0;
   for (int i = 0; i < oc; ++i) {
     const GOp op = p.ops[ob + i];
-    if (threadIdx.x == 0) s_stop = p.sc->status != 0;
+    // (an L2 read: other threads' pushes may have set the status with an atomic)
+    if (threadIdx.x == 0) s_stop = __hip_atomic_load(&p.sc->status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     __syncthreads();
     if (s_stop) break;
     const int32_t v = op.a;
@@ -670,15 +672,18 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
         p.W[sv] = ((uint64_t)(uint32_t)time << 32) | 0xffffffffull;
         p.stok[sv] = p.tokens[v];
         atomicAdd(&p.cnt[sv], kBig + (hi - lo));
-        const unsigned long long d = p.sc->draw;
-        for (int j = 0; j < od; ++j)
-          push_entry(p, obv + j, kGMarker | (uint32_t)sid, receive_time(p, d + j, time), pushes);
-        p.sc->draw = d + od;
+        s_draw = p.sc->draw;
       }
+      __syncthreads();
+      // the broadcast's pushes go to distinct channels: one thread per out-link, draw d + j
+      const unsigned long long d = s_draw;
+      for (int32_t j = threadIdx.x; j < od; j += blockDim.x)
+        push_entry(p, obv + j, kGMarker | (uint32_t)sid, receive_time(p, d + j, time), pushes);
+      if (threadIdx.x == 0) p.sc->draw = d + od;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0 && pushes) atomicAdd(&p.cpart[GC_PUSH], pushes);
+  if (pushes) atomicAdd(&p.cpart[GC_PUSH], pushes);
 }
 
 // ---------------------------------------------------------------------------
