@@ -553,11 +553,47 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
   }
 }
 
+// k_push with L lanes per node (small graphs: the grid is too small to hide latency with
+// one thread per node): lane jl owns out-channels jl, jl + L, ...; each channel gets the
+// node's broadcasts in creating-sender order, then the traffic send (queue.go:18-20), so
+// per-channel FIFO order is the same as one thread pushing them all.
+template <int L>
+__device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, int32_t ob, int32_t od, int ncre,
+                                       bool send, int32_t tok, int32_t tj, int32_t jl,
+                                       unsigned long long (&c)[2]) {
+  if (jl == 0) {
+    p.crn[v] = 0;
+    if (send) p.tokens[v] = tok - 1;  // SendTokens(v, out-link tj, 1): node.go:112-131
+  }
+  const int32_t lo = p.in_off[v];
+  for (int32_t j = jl; j < od; j += L) {
+    uint64_t q = p.hq[ob + j];
+    uint64_t prev = 0;
+    for (int r = 0; r < ncre; ++r) {
+      const uint64_t best = next_creation(p, lo, ncre, r, prev);
+      prev = best;
+      const int32_t s0 = (int32_t)(best >> 32);
+      const uint32_t sid = (uint32_t)best;
+      if (r == 0 && s0 < v) {
+        // v's own scan peeks the queues s0's broadcast made non-empty (sim.go:82-84)
+        const int pk = p.pick[v];
+        const int pj = (pk >> 6) == t ? (pk & 63) : 64;
+        if (j < pj && (uint32_t)q == kEmpty) ++c[1];
+      }
+      push_q(p, ob + j, q, kGMarker | sid, receive_time(p, broadcast_draw(p, s0) + (unsigned long long)j, t), c[0]);
+    }
+    if (send && j == tj) push_q(p, ob + j, q, 1u, receive_time(p, send_draw(p, v), t), c[0]);
+    p.hq[ob + j] = q;
+  }
+}
+
 // phase D: every node pushes onto its own out-channels -- the broadcasts of the local
 // snapshots created at it this tick (in creating-sender order), then its traffic send;
 // then the grid expands the local snapshots created at high in-degree nodes.
+template <int L>
 __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_t step) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int v = (int)(gid / L), jl = (int)(gid % L);
   int32_t ob = 0, od = 0, ncre = 0, tok = 0;
   if (v < p.n) {  // loaded while the status check is in flight
     ob = p.out_off[v];
@@ -571,8 +607,9 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_
     int32_t tj = -1;
     const bool send = traffic_send(p, step, v, od, tok, &tj);
     if (ncre) {
-      push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, c);
-    } else if (send) {
+      if constexpr (L == 1) push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, c);
+      else push_node_lanes<L>(p, t, v, ob, od, ncre, send, tok, tj, jl, c);
+    } else if (send && jl == 0) {
       // SendTokens(v, out-link j, 1): node.go:112-131 (one channel: no batching)
       p.tokens[v] = tok - 1;
       push_entry(p, ob + tj, 1u, receive_time(p, send_draw(p, v), t), c[0]);
@@ -775,11 +812,24 @@ int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream) {
   return hipGetLastError();
 }
 
+// k_push lanes per node: graphs under kLanesBelow nodes (fewer than ~1 wave per SIMD at one
+// thread per node) push with kPushLanes threads per node.
+constexpr int kPushLanes = 8;
+constexpr int32_t kLanesBelow = 1 << 18;
+void launch_push(const GParams& p, int32_t t, hipStream_t s) {
+  if (p.n < kLanesBelow) {
+    const int64_t m = (int64_t)p.n * kPushLanes;
+    hipLaunchKernelGGL(k_push<kPushLanes>, dim3((unsigned)((m + kGThreads - 1) / kGThreads)), dim3(kGThreads), 0, s, p, t, t);
+  } else {
+    hipLaunchKernelGGL(k_push<1>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t, t);
+  }
+}
+
 int cg_launch_sends(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_tally, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
-  hipLaunchKernelGGL(k_push, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t, t);
+  launch_push(p, t, s);
   return hipGetLastError();
 }
 
@@ -788,7 +838,7 @@ int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipLaunchKernelGGL(k_pick, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
   hipLaunchKernelGGL(k_marker, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
-  hipLaunchKernelGGL(k_push, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t, t);
+  launch_push(p, t, s);
   return hipGetLastError();
 }
 

@@ -91,7 +91,8 @@ def compare(g, o, check_counters=True):
     """Bit-exact comparison of a finished engine run with the oracle's."""
     assert g.status() == o.status, (g.status(), o.status)
     assert g.time() == o.time
-    ot = np.array([o.node_tokens()[k] for k in o.node_ids()], dtype=np.int64)
+    nt = o.node_tokens()  # (one call: it builds the whole map)
+    ot = np.array([nt[k] for k in o.node_ids()], dtype=np.int64)
     np.testing.assert_array_equal(g.node_tokens_array(), ot)
     if o.status in (0, O.HANG):
         assert g.num_snapshots == o.num_snapshots

@@ -65,6 +65,17 @@ def test_regular_traffic_vs_oracle(n, steps, seed):
     assert sums["digest"] == digest_from_oracle(o)
 
 
+def test_regular_one_thread_per_node_push_vs_oracle():
+    """A 2^18-node graph: k_push runs one thread per node (graphs below 2^18 nodes use 8
+    lanes per node), bit-exact against the oracle over 25 traffic steps (~2.5M pushes)."""
+    p = regular_program(1 << 18, steps=25, seed=4, snaps=((5, None), (5, 0), (17, None)))
+    g = engine_program(p)
+    o = oracle_program(p)
+    assert o.status == 0
+    compare(g, o)
+    assert g.checksums()["digest"] == digest_from_oracle(o)
+
+
 @pytest.mark.parametrize("n,steps,snaps", [(300, 300, 8), (300, 300, 24), (1500, 400, 48)])
 def test_powerlaw_overlapping_snapshots_vs_oracle(n, steps, snaps):
     """C5-shaped runs: skewed in-degree hub, one snapshot start per tick, long
