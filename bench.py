@@ -1,15 +1,20 @@
 #!/usr/bin/env python3
 """Benchmark: delivered packets/s of the batched Chandy-Lamport engine (BASELINE.json).
 
-A step = one pass of the hot path over one batch: every instance of the batch runs the
-whole event program (BASELINE config 2: 10nodes.top + 10nodes.events, 65,536 replicas
-per GPU, each with its own Go delay stream) from the initial topology to the end of the
-drain (test_common.go:79-140).  Inputs (topology, event program, delay schedule) are
-resident in HBM before timing; the timed region is K launches of the exec kernel.
+A step = one pass of the hot path over one batch: every instance runs the whole event
+program from the initial topology to the end of the drain (test_common.go:79-140).  The
+default batch is the north_star's: BASELINE config 3, 8nodes.top +
+8nodes-concurrent-snapshots.events x 2^20 instances, each with its own Go delay stream
+(instance i: rand.Seed(REFERENCE_SEED + i)).  Inputs (topology, event program, delay
+schedule) are resident in HBM before timing; the timed region is K launches of the exec
+kernel.  After timing, the batch checksums of the timed path are compared with the CPU
+oracle's values for the same instances (tests/golden/bench_sums.json): "parity".
 
-Multi-GPU: one process per GPU, each owning a disjoint instance range (seeds
-base + rank * I + i); instances are independent so there is no data-path collective
-("scaling": "weak").  RCCL all-reduces the batch checksums once, after timing.
+Multi-GPU: one process per GPU; the fixed 2^20-instance batch is split into disjoint
+instance ranges (rank r: instances [r*I/N, (r+1)*I/N), seeds base + global index), so
+there is no data-path collective ("scaling": "strong"); RCCL all-reduces the batch
+checksums once, after timing.  --config c2 is BASELINE config 2 (10nodes x 65,536);
+c4/c5 are the large-graph configs (one simulation per GPU, replicas).
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §6 for the byte model behind "roofline".
 """
@@ -28,12 +33,15 @@ PKG = "chandy-lamport-distributed-snapshot-algorithm_amd"
 TEST_DATA = os.path.join(ROOT, "tests", "golden", "test_data")
 
 CONFIGS = {
-    # BASELINE.json configs[1]: the headline single-GPU workload
+    # BASELINE.json configs[2] -- the north_star's batch and the default bench line:
+    # 2^20 instances in total, split over the ranks (strong scaling)
+    "c3": ("8nodes.top", "8nodes-concurrent-snapshots.events", 1 << 20,
+           "8nodes-concurrent x 1,048,576: 8nodes.top + 8nodes-concurrent-snapshots.events, "
+           "2^20 instances split over the GPUs, Go delay streams"),
+    # BASELINE.json configs[1]: 65,536 replicas (split over the GPUs likewise)
     "c2": ("10nodes.top", "10nodes.events", 65536,
-           "10nodes.top + 10nodes.events, 65,536 replicas per GPU, Go delay streams"),
-    # BASELINE.json configs[2]: 2^20 instances over 8 GPUs = 131,072 per GPU
-    "c3": ("8nodes.top", "8nodes-concurrent-snapshots.events", 131072,
-           "8nodes.top + 8nodes-concurrent-snapshots.events, 131,072 instances per GPU"),
+           "10nodes x 65,536: 10nodes.top + 10nodes.events, 65,536 replicas split over the GPUs, "
+           "Go delay streams"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -59,51 +67,88 @@ def b_alg(c, n_nodes):
         + 4 * n_nodes * c["completed"]
 
 
-def main():
+SIMDS = 256 * 4          # MI355X: 256 CUs x 4 SIMD-32 units (MI355X_MICROARCH.md)
+CLOCK_HZ = 2.4e9         # max engine clock (MI355X_MICROARCH.md)
+VALU_PEAK = SIMDS * CLOCK_HZ / 2   # wave64 VALU instructions/s: one per 2 cycles per SIMD-32
+FIXTURE = os.path.join(ROOT, "tests", "golden", "bench_sums.json")
+PARITY_KEYS = ("instances", "ok", "fatal", "other", "delivered", "snapshot_hash", "completed",
+               "cut_residual", "final_residual")
+
+
+def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + sorted(GRAPH_CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + sorted(GRAPH_CONFIGS))
     ap.add_argument("--graph-nodes", type=int, default=0, help="override the graph size (c4/c5)")
     ap.add_argument("--graph-steps", type=int, default=0, help="override the tick window (c4/c5)")
     ap.add_argument("--graph-fifo", type=int, default=0, help="override FIFO slots per channel (c4/c5)")
-    ap.add_argument("--instances", type=int, default=0, help="instances per GPU (default: config)")
+    ap.add_argument("--instances", type=int, default=0, help="instances in total (default: the config's batch)")
     ap.add_argument("--fifo-slots", type=int, default=0, help="LDS ring slots per channel (0 = automatic)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo for rehearsals")
+    ap.add_argument("--shared-device", action="store_true",
+                    help="every rank on cuda:0 (multi-rank rehearsal on a one-GPU box)")
+    return ap.parse_args()
 
+
+def init_dist(args, world, local_rank):
+    import torch
+    import torch.distributed as dist
+    device = 0 if args.shared_device else local_rank
+    if world > 1:
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.dist_backend, init_method="env://")
+    return device
+
+
+def profile_entry(cfg, instances):
+    """The matching committed rocprofv3 PMC summary (profiles/<round>_<cfg>_pmc.json)."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_pmc.json"))):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("instances") == instances:
+            best = (path, d)
+    return best
+
+
+def main():
+    args = parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config in GRAPH_CONFIGS:
         return bench_graph(args, rank, world, local_rank)
-    top, events, per_gpu, desc = CONFIGS[args.config]
+    top, events, total, desc = CONFIGS[args.config]
     if args.instances:
-        per_gpu = args.instances
+        total = args.instances
+    if total % world:
+        raise SystemExit(f"{total} instances do not split over {world} ranks")
+    per_rank = total // world
 
     import torch
     import torch.distributed as dist
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
+    device = init_dist(args, world, local_rank)
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(device)
 
     cl = importlib.import_module(PKG)
     cldist = importlib.import_module(PKG + ".dist")
-    _, seed_base = cldist.shard(per_gpu, rank, cl.REFERENCE_SEED)
-    sim = cl.ChandyLamportSim(per_gpu, device=local_rank, seed_base=seed_base,
+    _, seed_base = cldist.shard(per_rank, rank, cl.REFERENCE_SEED)
+    sim = cl.ChandyLamportSim(per_rank, device=device, seed_base=seed_base,
                               fifo_lds_slots=args.fifo_slots)
     sim.read_topology_file(os.path.join(TEST_DATA, top))
     sim.read_events_file(os.path.join(TEST_DATA, events))
     sim.flush()                      # uploads topology/program/delays, first full run
     counters = sim.counters(only_ok=False)
-    counters_ok = sim.counters(only_ok=True)
     n_nodes = sim.num_nodes
 
     for _ in range(args.warmup):
@@ -120,11 +165,26 @@ def main():
     elapsed = time.perf_counter() - t0
     k_total_ms, k_launches = sim.kernel_time()   # HIP events around each timed launch
 
+    # checksums of the LAST timed rerun (the timed path itself), all-reduced over ranks
     sums = sim.checksums()
-    t_max, red = cldist.reduce_results(elapsed, sums.tolist() + [counters_ok["pop_tok"] + counters_ok["pop_mk"]],
-                                       "cuda")   # RCCL all-reduce (max time, summed checksums)
+    recorded_ok = sim.counters(only_ok=True)["recorded"]
+    t_max, red = cldist.reduce_results(elapsed, sums.tolist() + [recorded_ok], coll_dev)
     tot = dict(zip(cl.SUM_NAMES, red[:len(cl.SUM_NAMES)]))
-    delivered_ok = red[-1]                       # packets of OK instances, all ranks
+    tot["recorded"] = red[len(cl.SUM_NAMES)]
+    delivered_ok = tot["delivered"]              # packets of OK instances, all ranks
+
+    parity, parity_note = None, "no fixture for this batch"
+    if os.path.exists(FIXTURE):
+        with open(FIXTURE) as f:
+            fx = json.load(f)
+        want = fx["batches"].get(args.config)
+        if want and want["instances"] == total and fx["seed_base"] == cl.REFERENCE_SEED:
+            w = want["sums"]
+            diff = {k: (tot[k], w[k]) for k in PARITY_KEYS + ("recorded",)
+                    if (tot[k] - w[k]) % (1 << 64) != 0}
+            parity = not diff
+            parity_note = "tests/golden/bench_sums.json (CPU oracle over every instance)" + \
+                ("" if parity else f"; mismatches {diff}")
 
     per_step = t_max / args.steps
     value = delivered_ok / per_step
@@ -134,15 +194,24 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(top, events, per_gpu, args.cpu_baseline_seconds)
+        cpu = cpu_baseline(top, events, total, args.cpu_baseline_seconds)
 
-    traffic = None
-    tr_path = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tr_path):
-        with open(tr_path) as f:
-            tr = json.load(f)
-        if tr.get("instances") == per_gpu and tr.get("fifo_slots") == args.fifo_slots:
-            traffic = tr.get("hbm_bytes_per_launch")
+    traffic, valu = None, None
+    prof = profile_entry(args.config, per_rank)
+    if prof is not None and args.fifo_slots == 0:
+        path, d = prof
+        c = d["counters"]
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            traffic = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+        if "SQ_INSTS_VALU" in c:
+            rate = c["SQ_INSTS_VALU"] / (avg_kernel_ms * 1e-3)
+            valu = {"achieved": rate, "peak": VALU_PEAK, "unit": "wave64 VALU instr/s",
+                    "frac": rate / VALU_PEAK, "insts_per_launch": c["SQ_INSTS_VALU"],
+                    "source": os.path.relpath(path, ROOT)}
+            if "SQ_WAVE_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
+                # SQ_WAVE_CYCLES counts quad-cycles summed over waves; GRBM over the 8 XCDs
+                valu["waves_per_simd"] = 4 * c["SQ_WAVE_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8) / SIMDS
+    hbm_frac = achieved / HBM_PEAK_GBS
 
     if rank == 0:
         line = {
@@ -154,21 +223,29 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": per_step * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic: reference test_data scenario, per-instance Go math/rand delay streams",
-            "config": {"workload": desc, "instances_per_gpu": per_gpu,
-                       "instances_total": per_gpu * world, "parallelism": f"instances sharded over {world} GPU(s)",
+            "config": {"workload": desc, "instances_total": total, "instances_per_gpu": per_rank,
+                       "parallelism": f"instances sharded over {world} GPU(s)",
                        "fifo_lds_slots": args.fifo_slots},
             "packets_per_step": delivered_ok,
+            "parity": parity,
+            "parity_ref": parity_note,
             "status": {"ok": tot["ok"], "fatal": tot["fatal"], "other": tot["other"]},
             "checks": {"cut_residual": tot["cut_residual"], "final_residual": tot["final_residual"],
-                       "snapshot_hash": tot["snapshot_hash"], "completed": tot["completed"]},
+                       "snapshot_hash": tot["snapshot_hash"], "completed": tot["completed"],
+                       "recorded": tot["recorded"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
+                         "frac": hbm_frac,
                          "traffic": traffic, "kernel": "cl_exec_kernel",
-                         "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg},
+                         "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg,
+                         "valu": valu,
+                         "binding_resource": (
+                             "per-wave issue latency (LDS round trips and dependent VALU chains at "
+                             "~3-4 resident waves per SIMD): neither the B_alg HBM fraction nor the "
+                             "VALU issue fraction is near 1; see DESIGN.md section 9")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -185,14 +262,13 @@ def b_alg_graph(c, n_nodes):
 def bench_graph(args, rank, world, local_rank):
     import torch
     import torch.distributed as dist
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
+    device = init_dist(args, world, local_rank)
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(device)
 
     clg = importlib.import_module(PKG + ".graph")
     cldist = importlib.import_module(PKG + ".dist")
@@ -205,7 +281,7 @@ def bench_graph(args, rank, world, local_rank):
     rs = seed + 1000 * rank           # replica seeds: delays, traffic, snapshot placement
     snap_nodes = [(clg.counter_hash(rs + 3, i, 1) * n) >> 64 for i in range(len(snap_steps))]
 
-    g = clg.GraphSim(device=local_rank, fifo_slots=fifo, max_snapshots=max(len(snap_steps), 1))
+    g = clg.GraphSim(device=device, fifo_slots=fifo, max_snapshots=max(len(snap_steps), 1))
     if cfg["kind"] == "regular":
         g.generate_regular(n, cfg["degree"], cfg["tokens"], seed)
     else:
@@ -236,7 +312,7 @@ def bench_graph(args, rank, world, local_rank):
     sums = g.checksums()
     status = g.status()
     vals = [sums[k] for k in clg.GSUM_NAMES]
-    t_max, red = cldist.reduce_results(elapsed, vals, "cuda")
+    t_max, red = cldist.reduce_results(elapsed, vals, coll_dev)
     tot = dict(zip(clg.GSUM_NAMES, red))
     per_step = t_max / args.steps
     value = tot["delivered"] / per_step if tot["ok"] == world else 0.0
@@ -319,28 +395,50 @@ def cpu_baseline_graph(g, cfg, n, steps, snap_steps, snap_nodes, rs, budget_s):
                       f"thread -- not the Go reference (no Go toolchain in the image)"}
 
 
+def host_cpu():
+    """(threads to use, CPU model, logical CPUs of the machine).  The GPU box grants a
+    share of its host cores per GPU (OMP_NUM_THREADS there); os.cpu_count() shows the
+    whole machine, so the pool is the affinity set capped by that share."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(avail, share) if share > 0 else avail
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return max(threads, 1), model, os.cpu_count()
+
+
 def cpu_baseline(top, events, n_total, budget_s):
-    """The CPU oracle (C restatement, one simulation per thread) on the same instances
-    (same seeds), repeated in passes until about budget_s of CPU work has run."""
+    """The CPU oracle (C restatement, one simulation per thread) over the SAME instance
+    set as the timed batch (instances 0..n_total-1, same seeds), with the topology and
+    events parsed once outside the timed region; repeated in passes until about
+    budget_s of wall time has run."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads, model, ncpu = host_cpu()
     t_text = open(os.path.join(TEST_DATA, top)).read()
     e_text = open(os.path.join(TEST_DATA, events)).read()
-    probe = min(n_total, 4096)
-    secs, st, _, cnt, _ = O.run_batch(t_text, e_text, probe, threads=threads)
-    sample = int(min(n_total, max(probe, probe / max(secs, 1e-6) * budget_s)))
     total_s, total_pkts, passes = 0.0, 0, 0
     while passes == 0 or total_s < budget_s:
-        secs, st, _, cnt, _ = O.run_batch(t_text, e_text, sample, threads=threads)
+        secs, st, _, cnt, _ = O.run_batch_prepared(t_text, e_text, n_total, seed_base=O.REFERENCE_SEED,
+                                                   threads=threads, want_hash=False)
         ok = st == 0
         total_pkts += int((cnt[ok, 2] + cnt[ok, 3]).sum())
         total_s += secs
         passes += 1
     return {"value": total_pkts / total_s, "unit": "packets/s", "cores": threads, "kind": "port",
-            "sample": f"{passes} pass(es) over the first {sample} of {n_total} instances (same seeds), "
-                      f"{total_s:.1f} s; CPU restatement in C (oracle/cl_oracle.c), one simulation per "
-                      f"thread -- not the Go reference (no Go toolchain in the image)"}
+            "cpu_model": model, "host_logical_cpus": ncpu,
+            "sample": f"{passes} pass(es) over all {n_total} instances of the timed batch (same seeds), "
+                      f"{total_s:.1f} s of simulation wall time on {threads} threads; topology and events "
+                      f"parsed once outside the timed region; CPU restatement in C (oracle/cl_oracle.c), "
+                      f"one simulation per thread at a time -- not the Go reference (no Go toolchain "
+                      f"in the image)"}
 
 
 if __name__ == "__main__":

@@ -35,6 +35,7 @@ constexpr uint32_t kOpen = 0xffffffffu;
 constexpr int32_t kBig = 1 << 30;
 constexpr int32_t kGMaxOutDegree = 64;  // non-empty out-channel bitmask per node (u64)
 constexpr int32_t kGThreads = 256;      // threads (= nodes) per pick / marker / push block
+constexpr int32_t kPushLanes = 8;       // k_push threads per node on small graphs
 constexpr int32_t kGStatusHistOverflow = 6;
 // A local snapshot created at a node of in-degree above this is expanded over its
 // in-links by the whole k_push grid instead of by the creating lane.
@@ -101,7 +102,7 @@ struct GParams {
   uint32_t traffic_thresh;
   int64_t traffic_steps;
   int32_t n_pblocks;  // node blocks = ceil(n / kGThreads)
-  int32_t pad0;
+  int32_t push_lanes;  // k_push threads per node: 0 = automatic, else forced (1 or kPushLanes)
   // topology (out-CSR channel order = (src rank, dest rank); in-CSR by (dest, src))
   const int32_t* out_off;   // [n+1]
   const int2* route;        // [e] channel c: (dest rank, in-CSR position)

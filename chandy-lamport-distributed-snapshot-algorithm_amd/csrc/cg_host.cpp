@@ -127,6 +127,7 @@ struct cl_graph {
   uint64_t traffic_seed = 0;
   uint32_t traffic_thresh = 0;
   int64_t traffic_steps = 0;
+  int32_t push_lanes = 0;  // k_push lanes per node: 0 automatic (cl_graph_set_push_lanes)
 
   // ---- program ---------------------------------------------------------------
   std::vector<ProgOp> prog;
@@ -442,6 +443,7 @@ struct cl_graph {
     p.traffic_thresh = traffic_thresh;
     p.traffic_steps = traffic_steps;
     p.n_pblocks = (n + kGThreads - 1) / kGThreads;
+    p.push_lanes = push_lanes;
     p.out_off = d_out_off.p;
     p.route = d_route.p;
     p.in_off = d_in_off.p;
@@ -509,9 +511,10 @@ struct cl_graph {
     return CL_OK;
   }
 
-  // test_common.go:123-137: tick until all started snapshots completed, then +6.
-  int run_drain() {
-    std::vector<int32_t> ct((size_t)std::max(n_sids, 1));
+  // test_common.go:123-137: tick until the snapshots started before this drain (sids
+  // [0, n_before)) have completed, then +6.  Later snapshots are not waited for.
+  int run_drain(int32_t n_before) {
+    std::vector<int32_t> ct((size_t)std::max(n_before, 1));
     int64_t ticks = 0;
     for (;;) {
       int32_t st;
@@ -519,9 +522,9 @@ struct cl_graph {
       if (rc) return rc;
       if (st) return CL_OK;
       bool all = true;
-      if (n_sids) {
-        GHIP(hipMemcpy(ct.data(), d_ctick.p, (size_t)n_sids * sizeof(int32_t), hipMemcpyDeviceToHost));
-        for (int32_t s = 0; s < n_sids; ++s) all = all && ct[s] >= 0;
+      if (n_before) {
+        GHIP(hipMemcpy(ct.data(), d_ctick.p, (size_t)n_before * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int32_t s = 0; s < n_before; ++s) all = all && ct[s] >= 0;
       }
       if (all) break;
       if (ticks >= max_drain) {
@@ -572,7 +575,9 @@ struct cl_graph {
     }
     state_valid = false;
     size_t pend_begin = gop_cursor, pend_count = 0;
-    for (size_t i = begin; i < prog.size(); ++i) {
+    // a HANG freezes the run where the reference's drain would loop forever: later ops
+    // never execute (the oracle and the multi-instance engine stop there too)
+    for (size_t i = begin; i < prog.size() && !hang; ++i) {
       const ProgOp& op = prog[i];
       if (op.kind == P_SEND || op.kind == P_SNAP) {
         ++pend_count;
@@ -582,7 +587,7 @@ struct cl_graph {
           if ((rc = launch_tick())) return rc;
       } else if (op.kind == P_DRAIN) {
         if ((rc = flush_hostops(pend_begin, pend_count))) return rc;
-        if ((rc = run_drain())) return rc;
+        if ((rc = run_drain(op.a))) return rc;
       }
     }
     if ((rc = flush_hostops(pend_begin, pend_count))) return rc;
@@ -680,8 +685,8 @@ int cl_graph_add_node(cl_graph* g, const char* id, int64_t tokens) {
   if (!id) return gerr(CL_E_INVALID, "null id");
   if (g->id_index.count(id)) return gerr(CL_E_DUPLICATE_NODE, "node %s already exists", id);
   if (tokens < 0 || tokens > INT32_MAX) return gerr(CL_E_LIMIT, "token count out of range");
+  if (g->total_tokens + tokens > INT32_MAX) return gerr(CL_E_LIMIT, "total tokens exceed int32");
   g->total_tokens += tokens;
-  if (g->total_tokens > INT32_MAX) return gerr(CL_E_LIMIT, "total tokens exceed int32");
   g->id_index[id] = (int)g->ids.size();
   g->ids.emplace_back(id);
   g->init_tokens.push_back(tokens);
@@ -850,6 +855,23 @@ int cl_graph_set_limits(cl_graph* g, int32_t fifo_slots, int32_t max_snapshots, 
   return CL_OK;
 }
 
+int cl_graph_set_push_lanes(cl_graph* g, int32_t lanes) {
+  G_CHECK(g);
+  if (lanes != 0 && lanes != 1 && lanes != kPushLanes)
+    return gerr(CL_E_INVALID, "push lanes must be 0 (automatic), 1 or %d", kPushLanes);
+  g->push_lanes = lanes;
+  return CL_OK;
+}
+
+int cl_graph_node_id_length(cl_graph* g, int32_t rank, int32_t* len) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  if (rank < 0 || rank >= g->n || !len) return gerr(CL_E_INVALID, "bad rank or output");
+  *len = (int32_t)g->node_id(rank).size();
+  return CL_OK;
+}
+
 int cl_graph_set_delay_hash(cl_graph* g, uint64_t seed) {
   G_CHECK(g);
   g->delay_mode = 0;
@@ -937,7 +959,7 @@ int cl_graph_drain(cl_graph* g) {
   G_CHECK(g);
   int rc = g->freeze();
   if (rc) return rc;
-  g->prog.push_back(ProgOp{P_DRAIN, 0, 0, 0});
+  g->prog.push_back(ProgOp{P_DRAIN, g->n_sids, 0, 0});  // waits for the snapshots started so far
   return CL_OK;
 }
 

@@ -813,11 +813,11 @@ int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream) {
 }
 
 // k_push lanes per node: graphs under kLanesBelow nodes (fewer than ~1 wave per SIMD at one
-// thread per node) push with kPushLanes threads per node.
-constexpr int kPushLanes = 8;
+// thread per node) push with kPushLanes threads per node; p.push_lanes forces either path
+// (cl_graph_set_push_lanes: the exact-match tests run both on the same graphs).
 constexpr int32_t kLanesBelow = 1 << 18;
 void launch_push(const GParams& p, int32_t t, hipStream_t s) {
-  if (p.n < kLanesBelow) {
+  if (p.push_lanes ? p.push_lanes == kPushLanes : p.n < kLanesBelow) {
     const int64_t m = (int64_t)p.n * kPushLanes;
     hipLaunchKernelGGL(k_push<kPushLanes>, dim3((unsigned)((m + kGThreads - 1) / kGThreads)), dim3(kGThreads), 0, s, p, t, t);
   } else {

@@ -41,6 +41,8 @@ def glib():
             "cl_graph_num_channels": [vp, vp],
             "cl_graph_channels": [vp, vp, vp],
             "cl_graph_node_id": [vp, i32, vp, i32],
+            "cl_graph_node_id_length": [vp, i32, vp],
+            "cl_graph_set_push_lanes": [vp, i32],
             "cl_graph_set_limits": [vp, i32, i32, i64],
             "cl_graph_set_delay_hash": [vp, u64],
             "cl_graph_set_delay_go_seed": [vp, i64],
@@ -142,6 +144,11 @@ class GraphSim:
     def set_traffic(self, seed, threshold, steps):
         _check(self._L.cl_graph_set_traffic(self._h, seed, threshold, steps))
 
+    def set_push_lanes(self, lanes):
+        """Force the push kernel's lanes per node (0 automatic, 1 or 8): diagnostics and
+        tests -- results are identical on either path."""
+        _check(self._L.cl_graph_set_push_lanes(self._h, lanes))
+
     # ---- events -------------------------------------------------------------------------
     def ProcessEvent(self, event):                  # sim.go:58
         if isinstance(event, PassTokenEvent):
@@ -227,10 +234,16 @@ class GraphSim:
 
     def node_ids(self):
         if self._ids is None:
-            buf = C.create_string_buffer(64)
+            cap = 64
+            buf = C.create_string_buffer(cap)
             out = []
             for r in range(self.num_nodes):
-                _check(self._L.cl_graph_node_id(self._h, r, buf, 64))
+                rc = self._L.cl_graph_node_id(self._h, r, buf, cap)
+                if rc == -7:                             # longer id: size the buffer to it
+                    cap = self._get(self._L.cl_graph_node_id_length, C.c_int32, r) + 1
+                    buf = C.create_string_buffer(cap)
+                    rc = self._L.cl_graph_node_id(self._h, r, buf, cap)
+                _check(rc)
                 out.append(buf.value.decode())
             self._ids = out
         return self._ids

@@ -75,8 +75,10 @@ int cl_graph_num_nodes(cl_graph* g, int32_t* n);
 int cl_graph_num_channels(cl_graph* g, int64_t* n);
 /* src[c], dst[c] ranks of every channel, channel order */
 int cl_graph_channels(cl_graph* g, int32_t* src, int32_t* dst);
-/* node id of a rank, NUL-terminated into buf[cap] */
+/* node id of a rank, NUL-terminated into buf[cap] (CL_E_LIMIT if cap <= its length) */
 int cl_graph_node_id(cl_graph* g, int32_t rank, char* buf, int32_t cap);
+/* length of a rank's node id (bytes, without the NUL): size buf for cl_graph_node_id */
+int cl_graph_node_id_length(cl_graph* g, int32_t rank, int32_t* len);
 
 /* ---- configuration (before the first flush) -------------------------------- */
 /* fifo_slots: ring slots per channel (power of two, 2..32768; deeper -> FIFO_OVERFLOW
@@ -94,6 +96,10 @@ int cl_graph_set_delay_schedule(cl_graph* g, const uint8_t* delays, int64_t n);
  * with out-links sends ONE token when (uint32)cl_counter_hash(seed, k, rank) <
  * threshold, on out-link ((hash >> 32) * outdeg) >> 32 (SendTokens node.go:112-131). */
 int cl_graph_set_traffic(cl_graph* g, uint64_t seed, uint32_t threshold, int64_t steps);
+/* Diagnostic override of the push kernel's lanes per node: 0 = automatic (8 lanes below
+ * 2^18 nodes, else 1), 1 or 8 = forced.  Results are identical either way; the tests run
+ * both paths on the same graphs. */
+int cl_graph_set_push_lanes(cl_graph* g, int32_t lanes);
 
 /* ---- events ------------------------------------------------------------------ */
 int cl_graph_send_tokens(cl_graph* g, const char* src, const char* dest, int64_t n);  /* sim.go:58-62 */
@@ -101,8 +107,10 @@ int cl_graph_send_tokens_rank(cl_graph* g, int32_t src, int32_t dest, int64_t n)
 int cl_graph_start_snapshot(cl_graph* g, const char* node, int32_t* out_sid);         /* sim.go:105 */
 int cl_graph_start_snapshot_rank(cl_graph* g, int32_t node, int32_t* out_sid);
 int cl_graph_tick(cl_graph* g, int32_t n);                                             /* sim.go:71 */
-/* test_common.go:123-137: tick until every started snapshot completed, then
- * maxDelay+1 more ticks.  Host-driven (checks completion between ticks). */
+/* test_common.go:123-137: tick until every snapshot started before this call has
+ * completed, then maxDelay+1 more ticks.  Host-driven (checks completion between
+ * ticks).  If it exceeds max_drain_ticks the run gets CL_INST_HANG and freezes: later
+ * program ops do not execute. */
 int cl_graph_drain(cl_graph* g);
 int cl_graph_read_events_text(cl_graph* g, const char* text, int32_t* n_snapshots); /* test_common.go:79-140 */
 int cl_graph_read_events_file(cl_graph* g, const char* path, int32_t* n_snapshots);

@@ -61,6 +61,7 @@ def lib():
             "orc_go_intn_seq": (None, [i64, i32, i64, vp]),
             "orc_run_batch": (C.c_double, [cp, cp, i64, vp, i64, i64, i64, C.c_int,
                                            vp, vp, vp, vp]),
+            "orc_run_batch_prepared": (C.c_double, [cp, cp, i64, i64, i64, C.c_int, vp, vp, vp, vp]),
             "orc_counter_hash": (C.c_uint64, [C.c_uint64, C.c_uint64, C.c_uint64]),
             "orc_counter_delay": (C.c_int, [C.c_uint64, C.c_uint64]),
             "orc_use_counter_hash": (None, [vp, C.c_uint64]),
@@ -285,6 +286,23 @@ def run_batch(top_text, events_text, n, sched=None, draws=0, seed_base=REFERENCE
     secs = lib().orc_run_batch(top_text.encode(), events_text.encode(), n, sp, draws, seed_base,
                                max_drain, threads, _ptr(status), _ptr(ticks), _ptr(counters),
                                _ptr(hashes))
+    if secs < 0:
+        raise RuntimeError("oracle batch failed (parse/API error)")
+    return secs, status, ticks, counters, hashes
+
+
+def run_batch_prepared(top_text, events_text, n, seed_base=REFERENCE_SEED, threads=1,
+                       max_drain=MAX_DRAIN_TICKS, want_hash=True):
+    """Like run_batch with Go seeds, but the topology and events are parsed once and
+    each thread resets one simulator per instance; the returned seconds cover the
+    simulations only (bench.py cpu_baseline).  hash is None unless want_hash."""
+    status = np.zeros(n, dtype=np.int32)
+    ticks = np.zeros(n, dtype=np.int64)
+    counters = np.zeros((n, 7), dtype=np.int64)
+    hashes = np.zeros(n, dtype=np.uint64) if want_hash else None
+    secs = lib().orc_run_batch_prepared(top_text.encode(), events_text.encode(), n, seed_base, max_drain,
+                                        threads, _ptr(status), _ptr(ticks), _ptr(counters),
+                                        _ptr(hashes) if want_hash else None)
     if secs < 0:
         raise RuntimeError("oracle batch failed (parse/API error)")
     return secs, status, ticks, counters, hashes

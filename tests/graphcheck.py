@@ -71,8 +71,9 @@ def oracle_program(p):
     return s
 
 
-def engine_program(p, device=0, run=True):
+def engine_program(p, device=0, run=True, lanes=0):
     g = clg.GraphSim(device=device, fifo_slots=p.fifo_slots)
+    g.set_push_lanes(lanes)
     g.set_topology(p.tokens, p.src, p.dst, id_width=p.width())
     g.set_delay_hash(p.delay_seed)
     g.set_traffic(p.traffic_seed, p.thresh, p.traffic_steps)

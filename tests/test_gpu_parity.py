@@ -234,3 +234,89 @@ def test_send_groups_with_midgroup_fatals(seed, tlo, thi):
         compare_instance(sim, i, ref, status=status, times=times)
         if status[i] == cl.INST_FATAL_INSUFFICIENT_TOKENS:
             assert sim.node_tokens(i) == ref.node_tokens(), f"instance {i}: frozen balances differ"
+
+
+@pytest.mark.parametrize("cfg", [("10nodes.top", "10nodes.events", 65536, None),
+                                 ("8nodes.top", "8nodes-concurrent-snapshots.events", 131072, None),
+                                 ("10nodes.top", "10nodes.events", 4096, 2),
+                                 ("8nodes.top", "8nodes-concurrent-snapshots.events", 8192, 2)],
+                         ids=["C2_x65536", "C3_x131072", "C2_spill_x4096", "C3_spill_x8192"])
+def test_rerun_equals_flush_and_oracle(cfg):
+    """The benchmark's timed path: cl_rerun replays the program from the initial state
+    with the kernel prologue resetting completion ticks and HBM spill-ring heads (no fill
+    launch).  Three reruns after the first flush must reproduce the flush and the oracle
+    exactly -- statuses, times, batch checksums, and sampled instances in full."""
+    top, events, n, slots = cfg
+    sim = engine_run(top, events, n, fifo_lds_slots=slots)
+    first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
+    _, st, ticks, cnt, hashes = oracle_batch(top, events, n, threads=16)
+    want = batch_sums_from_oracle(st, cnt, hashes)
+    for r in range(3):
+        sim.rerun()
+        sim.synchronize()
+        status, times, sums = sim.status(), sim.time(), sim.checksums()
+        assert np.array_equal(status, first[0]) and np.array_equal(status, st), f"rerun {r}: status"
+        assert np.array_equal(times, first[1]), f"rerun {r}: times"
+        assert np.array_equal(times[st == 0], ticks[st == 0]), f"rerun {r}: times vs oracle"
+        assert np.array_equal(sums, first[2]), f"rerun {r}: checksums"
+        got = dict(zip(cl.SUM_NAMES, sums.tolist()))
+        for k, v in want.items():
+            assert got[k] == v, f"rerun {r} {k}: engine {got[k]} vs oracle {v}"
+        assert got["cut_residual"] == 0 and got["final_residual"] == 0
+    rng = np.random.default_rng(11)
+    for i in np.concatenate([[0, n - 1], rng.choice(n, 24, replace=False)]):
+        compare_instance(sim, int(i), oracle_run(top, events, seed=O.REFERENCE_SEED + int(i)),
+                         status=status, times=times)
+
+
+def test_headline_batch_2p20_matches_fixture():
+    """The north_star batch itself (BASELINE config 3, 2^20 instances on one GPU): the
+    batch checksums of a flush and of a rerun equal the oracle's values over every
+    instance (tests/golden/bench_sums.json, tools/gen_bench_fixture.py)."""
+    import json
+    fx = json.load(open(os.path.join(os.path.dirname(TEST_DATA), "bench_sums.json")))
+    want = fx["batches"]["c3"]["sums"]
+    n = fx["batches"]["c3"]["instances"]
+    assert n == 1 << 20 and fx["seed_base"] == O.REFERENCE_SEED
+    sim = engine_run("8nodes.top", "8nodes-concurrent-snapshots.events", n)
+    for rnd in range(2):
+        got = dict(zip(cl.SUM_NAMES, sim.checksums().tolist()))
+        got["recorded"] = sim.counters(only_ok=True)["recorded"]
+        for k in want:
+            assert (got[k] - want[k]) % (1 << 64) == 0, f"pass {rnd} {k}: engine {got[k]} vs oracle {want[k]}"
+        sim.rerun()
+        sim.synchronize()
+
+
+def test_two_event_texts_and_snapshot_after_drain():
+    """Two readEventsFile calls on one batch, then a snapshot after the last drain and
+    more ticks: every instance equals the oracle running the same calls; a rerun
+    replays the whole program identically."""
+    top = "4\nA 10\nB 10\nC 10\nD 10\nA B\nB C\nC D\nD A\nB A\nC B\n"
+    ev1 = "send A B 3\nsnapshot A\ntick 2\nsend C D 1\n"
+    ev2 = "snapshot C\nsend B A 2\ntick 3\nsnapshot D\n"
+    n = 128
+    sim = cl.ChandyLamportSim(n)
+    sim.read_topology_text(top)
+    sim.read_events_text(ev1)
+    sim.flush()
+    sim.read_events_text(ev2)
+    sim.StartSnapshot("B")
+    sim.Tick(12)
+    sim.flush()
+    first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
+    refs = []
+    for i in range(n):
+        o = O.OracleSim()
+        o.seed_go(O.REFERENCE_SEED + i)
+        assert o.read_topology_text(top) == 0
+        if o.read_events_text(ev1) == 0 and o.read_events_text(ev2) == 0:
+            o.start_snapshot("B")
+            for _ in range(12):
+                o.tick()
+        refs.append(o)
+        compare_instance(sim, i, o, status=first[0], times=first[1])
+    sim.rerun()
+    sim.synchronize()
+    assert np.array_equal(sim.status(), first[0]) and np.array_equal(sim.time(), first[1])
+    assert np.array_equal(sim.checksums(), first[2])

@@ -76,12 +76,14 @@ def test_regular_one_thread_per_node_push_vs_oracle():
     assert g.checksums()["digest"] == digest_from_oracle(o)
 
 
+@pytest.mark.parametrize("lanes", [0, 1, 8])
 @pytest.mark.parametrize("n,steps,snaps", [(300, 300, 8), (300, 300, 24), (1500, 400, 48)])
-def test_powerlaw_overlapping_snapshots_vs_oracle(n, steps, snaps):
+def test_powerlaw_overlapping_snapshots_vs_oracle(n, steps, snaps, lanes):
     """C5-shaped runs: skewed in-degree hub, one snapshot start per tick, long
-    recording logs, most snapshots still in flight at the end."""
+    recording logs, most snapshots still in flight at the end.  lanes forces the push
+    kernel's one-thread-per-node path (1) or its 8-lane path (8); 0 = automatic."""
     p = powerlaw_program(n, steps, snaps, fifo_slots=512)
-    g = engine_program(p)
+    g = engine_program(p, lanes=lanes)
     o = oracle_program(p)
     compare(g, o)
     assert g.checksums()["digest"] == digest_from_oracle(o)
@@ -93,7 +95,7 @@ def _random_graph(rng, n):
 
 
 def _random_events_run(rng, n, src, dst, gseed, n_events, drain=500, tokens=(0, 50),
-                       link_sends=False):
+                       link_sends=False, lanes=0):
     ids = [f"n{r}" for r in rng.permutation(n)]
     top = f"{n}\n" + "".join(f"{ids[r]} {int(rng.integers(*tokens))}\n" for r in range(n)) + \
         "".join(f"{ids[a]} {ids[b]}\n" for a, b in zip(src, dst))
@@ -118,6 +120,7 @@ def _random_events_run(rng, n, src, dst, gseed, n_events, drain=500, tokens=(0, 
     if os.environ.get("CG_ORACLE_ONLY"):  # sizing aid on a CPU host
         return o
     g = clg.GraphSim(max_drain_ticks=drain)
+    g.set_push_lanes(lanes)
     g.read_topology_text(top)
     g.set_delay_go_seed(gseed)
     g.read_events_text(events)
@@ -137,16 +140,94 @@ def test_random_host_events_vs_oracle(seed):
     _random_events_run(rng, n, src, dst, O.REFERENCE_SEED + seed, int(rng.integers(5, 40)))
 
 
+@pytest.mark.parametrize("lanes", [0, 1, 8])
 @pytest.mark.parametrize("n,deg,seed", [(24, 23, 0), (70, 40, 1), (100, 62, 2)])
-def test_high_out_degree_vs_oracle(n, deg, seed):
+def test_high_out_degree_vs_oracle(n, deg, seed, lanes):
     """Dense digraphs: broadcasts over out-degrees up to 62 (k_push pushes them in chunks
-    of 8 channels), and one pick block whose out-channels exceed k_pick's LDS stage
-    (3,072 head words; n=70/100 have 2,800 / 6,200), so the fallback reads HBM."""
+    of 8 channels: multi-chunk and partial tail chunks), and one pick block whose
+    out-channels exceed k_pick's LDS stage (3,072 head words; n=70/100 have 2,800 /
+    6,200), so the fallback reads HBM.  Both push paths (lanes 1 and 8) are forced."""
     rng = np.random.default_rng(100 + seed)
     src = np.repeat(np.arange(n), deg)
     dst = np.concatenate([rng.choice(np.delete(np.arange(n), v), deg, replace=False) for v in range(n)])
     _random_events_run(rng, n, src.astype(np.int32), dst.astype(np.int32), O.REFERENCE_SEED + 77 + seed, 60,
-                       drain=4000, tokens=(100, 200), link_sends=True)
+                       drain=4000, tokens=(100, 200), link_sends=True, lanes=lanes)
+
+
+@pytest.mark.parametrize("lanes", [1, 8])
+def test_hub_expansion_both_push_paths_vs_oracle(lanes):
+    """Power-law hubs with in-degree > 64 (the grid-wide expansion of k_push<1>) and
+    nodes of out-degree 9-10 (a partial second chunk), on both push paths."""
+    p = powerlaw_program(2000, 250, 16, seed=5, fifo_slots=512)
+    assert np.bincount(p.dst).max() > 64
+    g = engine_program(p, lanes=lanes)
+    o = oracle_program(p)
+    compare(g, o)
+    assert g.checksums()["digest"] == digest_from_oracle(o)
+
+
+def test_two_event_texts_and_snapshot_after_drain_vs_oracle():
+    """Two readEventsFile calls on one simulator (test_common.go:79-140 twice): the
+    second drain waits only for the snapshots started before it.  Then a rerun after
+    more events were appended (snapshot after the last drain, more ticks) replays the
+    whole program identically to the incremental run and to the oracle."""
+    top = "4\nA 10\nB 10\nC 10\nD 10\nA B\nB C\nC D\nD A\nB A\nC B\n"
+    ev1 = "send A B 3\nsnapshot A\ntick 2\nsend C D 1\n"
+    ev2 = "snapshot C\nsend B A 2\ntick 3\nsnapshot D\n"
+    for seed in range(6):
+        gseed = O.REFERENCE_SEED + 31 * seed
+        o = O.OracleSim()
+        o.seed_go(gseed)
+        assert o.read_topology_text(top) == 0
+        assert o.read_events_text(ev1) == 0 and o.read_events_text(ev2) == 0
+        g = clg.GraphSim()
+        g.read_topology_text(top)
+        g.set_delay_go_seed(gseed)
+        g.read_events_text(ev1)
+        g.flush()                    # incremental: first file executed on its own
+        g.read_events_text(ev2)
+        g.flush()
+        compare(g, o)
+        one = clg.GraphSim()         # both files in one flush
+        one.read_topology_text(top)
+        one.set_delay_go_seed(gseed)
+        one.read_events_text(ev1)
+        one.read_events_text(ev2)
+        one.flush()
+        compare(one, o)
+        # a snapshot after the last drain, then ticks: incremental == rerun == oracle
+        g.StartSnapshot("B")
+        g.Tick(12)
+        g.flush()
+        o.start_snapshot("B")
+        for _ in range(12):
+            o.tick()
+        compare(g, o)
+        first = (g.status(), g.time(), g.checksums())
+        g.rerun()
+        g.synchronize()
+        assert (g.status(), g.time(), g.checksums()) == first
+        compare(g, o)
+
+
+def test_hang_freezes_later_ops():
+    """A drain that never completes (a node without in-links) is HANG and freezes the
+    run: later events do not execute, as in the oracle."""
+    top = "3\nA 5\nB 5\nC 0\nA B\nB C\nC B\n"
+    o = O.OracleSim()
+    o.seed_go(O.REFERENCE_SEED)
+    assert o.read_topology_text(top) == 0
+    o.read_events_text("snapshot A\ntick 3\n", 50)
+    assert o.status == O.HANG
+    g = clg.GraphSim(max_drain_ticks=50)
+    g.read_topology_text(top)
+    g.set_delay_go_seed(O.REFERENCE_SEED)
+    g.read_events_text("snapshot A\ntick 3\n")
+    g.read_events_text("send B C 1\ntick 4\n")   # after the hang: never executed
+    g.flush()
+    assert g.status() == cl.INST_HANG
+    assert g.time() == o.time
+    assert g.node_tokens() == o.node_tokens()
 
 
 def test_rerun_and_incremental_equal_one_shot():

@@ -19,16 +19,22 @@ KAT = json.load(open(os.path.join(ROOT, "tests", "golden", "go_rng_kat.json")))
 
 
 def header_symbols():
-    text = open(os.path.join(ROOT, "include", "clsnap.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(cl_\w+)\(", text, re.M)))
+    """Every function declared in include/*.h."""
+    import glob
+    out = {}
+    for path in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))):
+        text = open(path).read()
+        for s in re.findall(r"^(?:int|const char\*|uint64_t)\s+(cl_\w+)\(", text, re.M):
+            out[s] = os.path.basename(path)
+    return out
 
 
 def test_library_exports_every_declared_symbol():
     L = cl.lib()
     syms = header_symbols()
-    assert len(syms) >= 40
-    for s in syms:
-        assert hasattr(L, s), f"{s} declared in include/clsnap.h but not exported"
+    assert len(syms) >= 80
+    for s, h in syms.items():
+        assert hasattr(L, s), f"{s} declared in include/{h} but not exported"
 
 
 def test_product_go_rand_kats():

@@ -32,7 +32,7 @@ def per_dispatch(paths):
 
 def main():
     rnd, cfg = sys.argv[1], sys.argv[2]
-    inst = int(sys.argv[3]) if len(sys.argv) > 3 else {"c2": 65536, "c3": 131072}[cfg]
+    inst = int(sys.argv[3]) if len(sys.argv) > 3 else {"c2": 65536, "c3": 1 << 20}[cfg]
     src = os.path.join(ROOT, "gpurun_out", f"pmc_{cfg}")
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
