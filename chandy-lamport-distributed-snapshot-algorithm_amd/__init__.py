@@ -95,6 +95,9 @@ def lib():
         "cl_node_tokens": [vp, i64, vp],
         "cl_snapshot_tick": [vp, i32, i64, vp],
         "cl_collect_snapshot": [vp, i32, i64, vp, vp, vp, i64],
+        "cl_poll_snapshot": [vp, i32, i64, i64, vp],
+        "cl_wait_snapshot": [vp, i32, i64, i64, i64, vp],
+        "cl_collect_snapshot_range": [vp, i32, i64, i64, vp, vp, vp, vp, i64],
         "cl_get_counters": [vp, i32, vp],
         "cl_get_checksums": [vp, vp],
         "cl_go_delay_schedule": [i64, i64, i64, vp],
@@ -222,8 +225,15 @@ class ChandyLamportSim:
         _check(self._L.cl_start_snapshot(self._h, node_id.encode(), C.byref(sid)))
         return sid.value
 
-    def CollectSnapshot(self, snapshot_id, instance=0):   # sim.go:134
-        """GlobalSnapshot of one instance, messages in (dest, src, delivery) order."""
+    def CollectSnapshot(self, snapshot_id, instance=0, timeout_ms=0):   # sim.go:134
+        """GlobalSnapshot of one instance, messages in (dest, src, delivery) order.
+
+        The reference blocks until the snapshot completes (sim.go:137-140): pass
+        timeout_ms=-1 for that (from a collector thread while another thread drives
+        the ticks), or a bound in ms; the default 0 raises ClSnapError(-9) at once if
+        the snapshot has not completed."""
+        if timeout_ms:
+            self.wait_snapshot(snapshot_id, instance, instance + 1, timeout_ms)
         n, ch = self.num_nodes, self.num_channels
         tok = np.zeros(n, dtype=np.int64)
         off = np.zeros(ch + 1, dtype=np.int64)
@@ -243,6 +253,43 @@ class ChandyLamportSim:
         msgs = [MsgSnapshot(ids[chans[c][0]], ids[chans[c][1]], int(msg[k]))
                 for c in order for k in range(off[c], off[c + 1])]
         return GlobalSnapshot(snapshot_id, token_map, msgs)
+
+    def poll_snapshot(self, snapshot_id, inst_lo=0, inst_hi=None):
+        """Instances of [inst_lo, inst_hi) in which the snapshot has completed (the
+        per-instance WaitGroup of sim.go:116-131); executes issued events, never ticks."""
+        hi = self.n_instances if inst_hi is None else inst_hi
+        v = C.c_int64(0)
+        _check(self._L.cl_poll_snapshot(self._h, snapshot_id, inst_lo, hi, C.byref(v)))
+        return v.value
+
+    def wait_snapshot(self, snapshot_id, inst_lo=0, inst_hi=None, timeout_ms=-1):
+        """Block until the snapshot has completed in every instance of [inst_lo,
+        inst_hi); woken by the driver thread's executions.  Raises ClSnapError(-9) on
+        timeout (timeout_ms >= 0)."""
+        hi = self.n_instances if inst_hi is None else inst_hi
+        v = C.c_int64(0)
+        _check(self._L.cl_wait_snapshot(self._h, snapshot_id, inst_lo, hi, timeout_ms, C.byref(v)))
+        return v.value
+
+    def collect_snapshot_range(self, snapshot_id, inst_lo=0, inst_hi=None):
+        """CollectSnapshot of many instances: (tokens[n, N] rank order, -1 where not
+        complete; complete[n]; offsets[n * C + 1]; messages) -- one CSR over
+        (instance, channel) with channels in (src rank, dest rank) order."""
+        hi = self.n_instances if inst_hi is None else inst_hi
+        k, n, ch = hi - inst_lo, self.num_nodes, self.num_channels
+        tok = np.zeros((k, n), dtype=np.int64)
+        done = np.zeros(k, dtype=np.int32)
+        off = np.zeros(k * ch + 1, dtype=np.int64)
+        cap = max(1024, 4 * k)
+        while True:
+            msg = np.zeros(cap, dtype=np.int64)
+            rc = self._L.cl_collect_snapshot_range(self._h, snapshot_id, inst_lo, hi, _p(tok), _p(done), _p(off),
+                                                   _p(msg), cap)
+            if rc == -7 and off[-1] > cap:
+                cap = int(off[-1])
+                continue
+            _check(rc)
+            return tok, done.astype(bool), off, msg[:off[-1]]
 
     # ---- drivers (test_common.go) -------------------------------------------
     def read_topology_file(self, path):           # test_common.go:29

@@ -14,10 +14,13 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <mutex>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -165,6 +168,14 @@ struct DevBuf {
 // cl_sim
 // ---------------------------------------------------------------------------
 struct cl_sim {
+  // Every ABI call on a sim holds `mu` (recursive: the drivers call the event entry
+  // points).  A collector thread may poll / wait / collect while the driver thread
+  // issues events and ticks (sim.go:134-173 runs CollectSnapshot on its own goroutine,
+  // test_common.go:106-108); `executed_cv` is signalled after every execution.
+  mutable std::recursive_mutex mu;
+  std::condition_variable_any executed_cv;
+  uint64_t exec_gen = 0;  // executions completed (flushes that ran ops)
+
   int64_t n_inst = 0;
   int64_t stride = 0;  // n_inst rounded up to the wave size
   int device = 0;
@@ -612,11 +623,40 @@ struct cl_sim {
   }
 
   int flush() {
+    bool ran = false;
     if (!frozen || executed != (int32_t)ops.size() || need_fresh) {
       int rc = launch(false, true);
       if (rc) return rc;
+      ran = true;
     }
-    return sync();
+    int rc = sync();
+    if (rc == CL_OK && ran) {
+      ++exec_gen;
+      executed_cv.notify_all();
+    }
+    return rc;
+  }
+
+  // Instances of [lo, hi) in which snapshot sid has completed, as of every event issued
+  // so far (pending events are executed; no tick is added).
+  int count_complete(int32_t sid, int64_t lo, int64_t hi, int64_t* n) {
+    int rc = flush();
+    if (rc) return rc;
+    const int32_t* t;
+    std::vector<int32_t> plane;
+    if (h_valid) {
+      t = h_snap_tick.data() + (size_t)sid * stride + lo;
+    } else {
+      plane.resize((size_t)(hi - lo));
+      if (hi > lo)
+        HIP_TRY(hipMemcpy(plane.data(), d_snap_tick.p + (size_t)sid * stride + lo, plane.size() * sizeof(int32_t),
+                          hipMemcpyDeviceToHost));
+      t = plane.data();
+    }
+    int64_t c = 0;
+    for (int64_t i = 0; i < hi - lo; ++i) c += t[i] >= 0;
+    *n = c;
+    return CL_OK;
   }
 
   int fetch() {
@@ -667,10 +707,9 @@ const char* cl_status_string(int32_t code) {
   }
 }
 
-#define SIM_CHECK(s)                                               \
-  do {                                                             \
-    if (!(s)) return set_err(CL_E_INVALID, "null cl_sim handle"); \
-  } while (0)
+#define SIM_CHECK(s)                                                \
+  if (!(s)) return set_err(CL_E_INVALID, "null cl_sim handle");  \
+  std::lock_guard<std::recursive_mutex> sim_lock_((s)->mu)
 
 int cl_sim_create(int64_t n_instances, cl_sim** out) {
   if (!out || n_instances <= 0) return set_err(CL_E_INVALID, "n_instances must be > 0");
@@ -682,6 +721,10 @@ int cl_sim_create(int64_t n_instances, cl_sim** out) {
 }
 
 int cl_sim_destroy(cl_sim* sim) {
+  if (sim) {
+    sim->mu.lock();  // no other thread may still be inside a call on this sim
+    sim->mu.unlock();
+  }
   delete sim;
   return CL_OK;
 }
@@ -1058,6 +1101,70 @@ int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens,
     }
   }
   msg_offsets[C] = m;
+  return fits ? CL_OK : set_err(CL_E_LIMIT, "msg_cap %lld < %lld messages", (long long)msg_cap, (long long)m);
+}
+
+int cl_poll_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t* n_complete) {
+  SIM_CHECK(sim);
+  if (!n_complete) return set_err(CL_E_INVALID, "null output");
+  if (sid < 0 || sid >= sim->n_sids || inst_lo < 0 || inst_hi > sim->n_inst || inst_lo > inst_hi)
+    return set_err(CL_E_INVALID, "snapshot/instance range out of range");
+  return sim->count_complete(sid, inst_lo, inst_hi, n_complete);
+}
+
+int cl_wait_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t timeout_ms,
+                     int64_t* n_complete) {
+  if (!sim) return set_err(CL_E_INVALID, "null cl_sim handle");
+  std::unique_lock<std::recursive_mutex> lk(sim->mu);
+  if (sid < 0 || sid >= sim->n_sids || inst_lo < 0 || inst_hi > sim->n_inst || inst_lo > inst_hi)
+    return set_err(CL_E_INVALID, "snapshot/instance range out of range");
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
+  for (;;) {
+    int64_t n = 0;
+    int rc = sim->count_complete(sid, inst_lo, inst_hi, &n);
+    if (rc) return rc;
+    if (n_complete) *n_complete = n;
+    if (n == inst_hi - inst_lo) return CL_OK;
+    const uint64_t gen = sim->exec_gen;
+    auto more = [&] { return sim->exec_gen != gen; };
+    if (timeout_ms < 0) {
+      sim->executed_cv.wait(lk, more);
+    } else if (!sim->executed_cv.wait_until(lk, deadline, more)) {
+      return set_err(CL_E_NOT_COMPLETE, "snapshot %d: %lld of %lld instances complete at the timeout", sid,
+                     (long long)n, (long long)(inst_hi - inst_lo));
+    }
+  }
+}
+
+int cl_collect_snapshot_range(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t* tokens,
+                              int32_t* complete, int64_t* msg_offsets, int64_t* msg_tokens, int64_t msg_cap) {
+  SIM_CHECK(sim);
+  if (sid < 0 || sid >= sim->n_sids || inst_lo < 0 || inst_hi > sim->n_inst || inst_lo > inst_hi)
+    return set_err(CL_E_INVALID, "snapshot/instance range out of range");
+  int rc = sim->fetch();
+  if (rc) return rc;
+  const size_t st = sim->stride;
+  const int n = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
+  int64_t m = 0;
+  bool fits = true;
+  for (int64_t i = inst_lo; i < inst_hi; ++i) {
+    const int64_t r = i - inst_lo;
+    const bool done = sim->h_snap_tick[(size_t)sid * st + i] >= 0;
+    if (complete) complete[r] = done ? 1 : 0;
+    if (tokens)
+      for (int v = 0; v < n; ++v) tokens[r * n + v] = done ? sim->h_snap_tok[((size_t)sid * st + i) * n + v] : -1;
+    for (int c = 0; c < C; ++c) {
+      if (msg_offsets) msg_offsets[r * C + c] = m;
+      if (!done) continue;
+      const uint32_t rec = sim->h_snap_rec[((size_t)sid * st + i) * C + c];
+      const uint32_t b = rec & 0xffffu, e = rec >> 16;
+      for (uint32_t k = b; k < e; ++k, ++m) {
+        if (m < msg_cap && msg_tokens) msg_tokens[m] = sim->hist[c][k];
+        else fits = false;
+      }
+    }
+  }
+  if (msg_offsets) msg_offsets[(inst_hi - inst_lo) * C] = m;
   return fits ? CL_OK : set_err(CL_E_LIMIT, "msg_cap %lld < %lld messages", (long long)msg_cap, (long long)m);
 }
 

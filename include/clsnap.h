@@ -18,8 +18,13 @@
  *     describes the most recent failure on the calling thread.
  *   - All buffers are caller-allocated; no pointer returned by the library is owned by
  *     the caller except where stated.
- *   - One host thread drives a cl_sim.  Event calls only append to the sim's event
- *     program; cl_flush() (or any result query) executes pending events on the GPU.
+ *   - One host thread drives a cl_sim (events, ticks, flush).  Event calls only append
+ *     to the sim's event program; cl_flush() (or any result query) executes pending
+ *     events on the GPU.  Every call holds the sim's lock, so other threads may call
+ *     cl_poll_snapshot / cl_wait_snapshot / cl_collect_snapshot* concurrently -- the
+ *     reference collects each snapshot on its own goroutine while the driver ticks
+ *     (test_common.go:106-108, sim.go:134-173).  Those calls execute events already
+ *     issued but never add a tick.
  *   - Node order everywhere is the reference's getSortedKeys order (common.go:135-146):
  *     lexicographic byte order of the node IDs ("rank").  Channel c is the c-th link in
  *     (src rank, dest rank) order -- the order Tick scans senders and out-links
@@ -164,6 +169,27 @@ int cl_snapshot_tick(cl_sim* sim, int32_t sid, int64_t inst, int32_t* tick);
 int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens,
                         int64_t* msg_offsets /* [num_channels + 1] */, int64_t* msg_tokens,
                         int64_t msg_cap);
+/* Completion of snapshot sid over instances [inst_lo, inst_hi) -- the global
+ * WaitGroup of sim.go:116-117,126-131 per instance: *n_complete = instances whose
+ * snapshot has completed after every event issued so far (pending events are executed,
+ * no tick is added).  Non-blocking apart from that execution. */
+int cl_poll_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t* n_complete);
+/* The blocking side of CollectSnapshot (sim.go:137-140): wait until snapshot sid has
+ * completed in every instance of [inst_lo, inst_hi).  The caller is a collector thread;
+ * it is woken after each execution of the driver's events (cl_flush, queries) and
+ * re-checks.  timeout_ms < 0 waits forever; on timeout returns CL_E_NOT_COMPLETE with
+ * *n_complete (may be NULL) set.  Never ticks. */
+int cl_wait_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t timeout_ms,
+                     int64_t* n_complete);
+/* CollectSnapshot (sim.go:134-173) of instances [inst_lo, inst_hi) at once:
+ * tokens[(i - inst_lo) * N + rank] (-1 for an instance whose snapshot has not
+ * completed, with complete[i - inst_lo] = 0; complete may be NULL); the recorded
+ * messages as ONE CSR over (instance, channel): the messages of instance i on channel c
+ * are msg_tokens[msg_offsets[r * C + c] .. msg_offsets[r * C + c + 1]), r = i - inst_lo,
+ * msg_offsets has (inst_hi - inst_lo) * C + 1 entries.  CL_E_LIMIT (offsets still
+ * written) if msg_cap is too small. */
+int cl_collect_snapshot_range(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t* tokens,
+                              int32_t* complete, int64_t* msg_offsets, int64_t* msg_tokens, int64_t msg_cap);
 /* Counters over instances (only_ok: restrict to CL_INST_OK instances). */
 int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out /* [CL_NUM_COUNTERS] */);
 /* Batch checksums computed on the GPU (see CL_SUM_*); all-reduce them across ranks. */
