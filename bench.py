@@ -54,9 +54,10 @@ GRAPH_CONFIGS = {
                desc="random 8-out regular digraph, 2^20 nodes, one snapshot under continuous token "
                     "traffic (p=1/4 per node per tick), 80 ticks"),
     "c5": dict(kind="powerlaw", n=100_000, targets=8, exponent=0.9, ring=True, tokens=100, steps=4100,
-               snap_steps=list(range(1, 4097)), fifo=8192, seed=30240,
+               snap_steps=list(range(1, 4097)), fifo=8192, seed=30240, drain=True,
                desc="power-law digraph (8 Zipf(0.9) targets + ring), 100k nodes, 4,096 overlapping "
-                    "snapshots (one start per tick), 4,100-tick window under continuous traffic"),
+                    "snapshots (one start per tick) under continuous traffic for 4,100 ticks, then "
+                    "readEventsFile's drain until every snapshot completed (+6 ticks)"),
 }
 
 
@@ -281,7 +282,8 @@ def bench_graph(args, rank, world, local_rank):
     rs = seed + 1000 * rank           # replica seeds: delays, traffic, snapshot placement
     snap_nodes = [(clg.counter_hash(rs + 3, i, 1) * n) >> 64 for i in range(len(snap_steps))]
 
-    g = clg.GraphSim(device=device, fifo_slots=fifo, max_snapshots=max(len(snap_steps), 1))
+    g = clg.GraphSim(device=device, fifo_slots=fifo, max_snapshots=max(len(snap_steps), 1),
+                     max_drain_ticks=1_000_000)
     if cfg["kind"] == "regular":
         g.generate_regular(n, cfg["degree"], cfg["tokens"], seed)
     else:
@@ -294,6 +296,8 @@ def bench_graph(args, rank, world, local_rank):
             g.start_snapshot_rank(int(snap_nodes[si]))
             si += 1
         g.Tick(1)
+    if cfg.get("drain"):
+        g.drain()                           # test_common.go:123-137, on the device
     g.flush()                               # allocates, uploads, first full run
     counters = g.counters()
     for _ in range(args.warmup):
@@ -346,7 +350,8 @@ def bench_graph(args, rank, world, local_rank):
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic: generated graph, counter-hash traffic and delay streams (seeded per rank)",
-            "config": {"workload": cfg["desc"], "nodes": n, "channels": g.num_channels, "ticks": steps,
+            "config": {"workload": cfg["desc"], "nodes": n, "channels": g.num_channels,
+                       "ticks": ticks // max(runs, 1), "traffic_ticks": steps,
                        "snapshots": len(snap_steps), "fifo_slots": fifo,
                        "parallelism": f"one replica per GPU, {world} GPU(s)"},
             "packets_per_step": tot["delivered"],

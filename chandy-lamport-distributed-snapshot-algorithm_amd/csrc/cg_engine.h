@@ -86,8 +86,16 @@ struct GScal {
   int32_t status;
   int32_t big_n;    // creations at high in-degree nodes this tick
   int32_t time;     // simulator time of the last tick that ran (sim.go:13)
-  int32_t pad;
+  int32_t skip;     // the drain is over (or hung): launched drain ticks do nothing
+  // device-side drain (test_common.go:123-137), evaluated by k_drain_ctl before each tick
+  int32_t dphase;   // 0 waiting for completions, 1 the maxDelay+1 extra ticks, 2 done, 3 hang
+  int32_t dleft;    // extra ticks left in phase 1
+  int32_t dticks;   // ticks spent waiting
+  int32_t dcur;     // first snapshot (< the drain's count) not yet complete
 };
+enum : int32_t { kDrainWait = 0, kDrainExtra = 1, kDrainDone = 2, kDrainHang = 3 };
+constexpr int32_t kTimeFromDevice = -1;
+constexpr int32_t kDrainExtraTicks = 6;  // maxDelay + 1 (test_common.go:135-137)  // tick argument: read the tick's time from GScal.time
 
 struct GParams {
   int32_t n, e;
@@ -142,6 +150,13 @@ struct GParams {
 // Launchers (cg_kernels.hip); return hipError_t as int.
 int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream);
 int cg_launch_tick(const GParams& p, int32_t t, void* stream);
+// Drain (test_common.go:123-137) on the device: reset the drain state for the snapshots
+// [0, n_before), then `ticks` x (k_drain_ctl + one tick whose time comes from GScal):
+// k_drain_ctl decides on the device whether the tick runs (waiting, then maxDelay+1 extra
+// ticks) or is skipped (drain over / hung), so the host checks only once per batch.
+int cg_launch_drain_begin(const GParams& p, void* stream);
+int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain, int32_t ticks, void* stream);
+int cg_launch_drain_end(const GParams& p, void* stream);  // normal ticks run again
 int cg_launch_sends(const GParams& p, int32_t t, void* stream);  // step-0 traffic
 int cg_launch_hostops(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream);
 // Recorded copies on channels still recording at the end (out[0] += ...).

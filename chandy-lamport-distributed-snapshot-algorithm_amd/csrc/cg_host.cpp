@@ -92,7 +92,6 @@ int digits(int64_t x) {
   return d;
 }
 
-constexpr int64_t kExtraDrainTicks = 6;  // maxDelay + 1 (test_common.go:135-137)
 constexpr int64_t kMaxGraphTime = (1 << 25) - 8;  // pick words hold (tick << 6) | out-index
 
 }  // namespace
@@ -512,33 +511,27 @@ struct cl_graph {
   }
 
   // test_common.go:123-137: tick until the snapshots started before this drain (sids
-  // [0, n_before)) have completed, then +6.  Later snapshots are not waited for.
+  // [0, n_before)) have completed, then +6.  Later snapshots are not waited for.  The
+  // loop runs on the device (k_drain_ctl before every tick decides whether it runs), so
+  // the host launches ticks in growing batches and reads the drain state once per batch.
   int run_drain(int32_t n_before) {
-    std::vector<int32_t> ct((size_t)std::max(n_before, 1));
-    int64_t ticks = 0;
+    int rc = k_err(cg_launch_drain_begin(P, stream));
+    if (rc) return rc;
+    const int32_t time0 = (int32_t)time;
+    int32_t batch = 8;
+    GScal sc;
     for (;;) {
-      int32_t st;
-      int rc = read_status(&st);
-      if (rc) return rc;
-      if (st) return CL_OK;
-      bool all = true;
-      if (n_before) {
-        GHIP(hipMemcpy(ct.data(), d_ctick.p, (size_t)n_before * sizeof(int32_t), hipMemcpyDeviceToHost));
-        for (int32_t s = 0; s < n_before; ++s) all = all && ct[s] >= 0;
-      }
-      if (all) break;
-      if (ticks >= max_drain) {
-        hang = true;
-        return CL_OK;
-      }
-      if ((rc = launch_tick())) return rc;
-      ++ticks;
+      if ((rc = k_err(cg_launch_drain_ticks(P, n_before, max_drain, batch, stream)))) return rc;
+      GHIP(hipMemcpyAsync(&sc, d_sc.p, sizeof sc, hipMemcpyDeviceToHost, stream));
+      GHIP(hipStreamSynchronize(stream));
+      if (sc.status || sc.dphase == kDrainDone || sc.dphase == kDrainHang) break;
+      batch = std::min(batch * 2, 256);
     }
-    for (int64_t i = 0; i < kExtraDrainTicks; ++i) {
-      int rc = launch_tick();
-      if (rc) return rc;
-    }
-    return CL_OK;
+    if (sc.dphase == kDrainHang) hang = true;
+    if (!sc.status) time = sc.time;  // (a frozen run reports the device time itself)
+    else time = std::max<int64_t>(time, sc.time);
+    run_ticks += std::max<int64_t>(0, time - time0);
+    return k_err(cg_launch_drain_end(P, stream));
   }
 
   // Execute program ops [executed, end) on the device; from scratch if `fresh`.

@@ -75,7 +75,7 @@ __device__ inline void block_count(const GParams& p, const int (&idx)[NV], unsig
 // kernel must not split a block at a barrier).
 __device__ inline bool block_frozen(const GParams& p) {
   __shared__ int s_frozen;
-  if (threadIdx.x == 0) s_frozen = p.sc->status;
+  if (threadIdx.x == 0) s_frozen = p.sc->status | p.sc->skip;
   __syncthreads();
   return s_frozen != 0;
 }
@@ -222,6 +222,63 @@ __device__ inline int expand_range(const GParams& p, int32_t t, int32_t s0, int3
 }
 
 // ---------------------------------------------------------------------------
+// device-side drain (test_common.go:123-137)
+// ---------------------------------------------------------------------------
+__global__ void k_drain_begin(GParams p) {
+  GScal* sc = p.sc;
+  sc->dphase = kDrainWait;
+  sc->dleft = 0;
+  sc->dticks = 0;
+  sc->dcur = 0;
+  sc->skip = 0;
+}
+
+// Before each drain tick (one thread): the reference's loop `select { case <-getSnapshots:
+// ...; default: sim.Tick() }` until every snapshot started before the drain was collected,
+// then maxDelay+1 more ticks.  Completion is checked before the tick, as the host loop did;
+// snapshot completions are permanent, so a cursor over [0, n_before) makes the check O(1)
+// amortized.  A run that needs more than max_drain waiting ticks hangs (status HANG on the
+// host) -- the reference would loop forever.
+__global__ void k_drain_ctl(GParams p, int32_t n_before, int32_t max_drain) {
+  GScal* sc = p.sc;
+  if (sc->status) {
+    sc->skip = 1;
+    return;
+  }
+  int32_t ph = sc->dphase;
+  if (ph == kDrainWait) {
+    int32_t c = sc->dcur;
+    while (c < n_before && p.ctick[c] >= 0) ++c;
+    sc->dcur = c;
+    if (c == n_before) {
+      ph = kDrainExtra;
+      sc->dleft = kDrainExtraTicks;
+    } else if (sc->dticks >= max_drain) {
+      sc->dphase = kDrainHang;
+      sc->skip = 1;
+      return;
+    } else {
+      sc->dticks += 1;
+      sc->time += 1;  // time++ of the tick that follows (sim.go:72)
+      sc->skip = 0;
+      return;
+    }
+  }
+  if (ph == kDrainExtra && sc->dleft > 0) {
+    sc->dleft -= 1;
+    sc->dphase = ph;
+    sc->time += 1;
+    sc->skip = 0;
+    return;
+  }
+  if (ph == kDrainExtra) ph = kDrainDone;
+  sc->dphase = ph;
+  sc->skip = 1;
+}
+
+__global__ void k_drain_end(GParams p) { p.sc->skip = 0; }
+
+// ---------------------------------------------------------------------------
 // reset
 // ---------------------------------------------------------------------------
 __global__ void k_reset(GParams p, const int32_t* init_tok) {
@@ -241,8 +298,9 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
 // ---------------------------------------------------------------------------
 // tick phase A: pick + deliver
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
+__global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
   __shared__ int s_m;
+  const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;  // drain ticks: set by k_drain_ctl
   // Head receiveTime words of the block's senders: the block's out-channels are one
   // contiguous CSR range, loaded once with coalesced loads (a lane-per-sender prefetch
   // touched 64 separate 64 B segments per wave instruction).  Channels past kStage
@@ -329,7 +387,8 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t t) {
 // ---------------------------------------------------------------------------
 // tick phase B: the markers delivered by pick block b's senders, and block b's tally
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t t) {
+__global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
+  const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;
   // the tally's inputs (node tokens after this tick's deliveries, out-degree) and the
   // block's marker count are loaded while the status check is in flight
   const int32_t sendbit = tally_send_bit(p, t);
@@ -591,7 +650,9 @@ __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, i
 // snapshots created at it this tick (in creating-sender order), then its traffic send;
 // then the grid expands the local snapshots created at high in-degree nodes.
 template <int L>
-__global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t t, int32_t step) {
+__global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int32_t sarg) {
+  const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;
+  const int32_t step = sarg != kTimeFromDevice ? sarg : t;  // the traffic of step t follows tick t
   const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int v = (int)(gid / L), jl = (int)(gid % L);
   int32_t ob = 0, od = 0, ncre = 0, tok = 0;
@@ -839,6 +900,29 @@ int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipLaunchKernelGGL(k_marker, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
   launch_push(p, t, s);
+  return hipGetLastError();
+}
+
+int cg_launch_drain_begin(const GParams& p, void* stream) {
+  hipLaunchKernelGGL(k_drain_begin, dim3(1), dim3(1), 0, (hipStream_t)stream, p);
+  return hipGetLastError();
+}
+
+int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain, int32_t ticks, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int32_t md = max_drain > INT32_MAX ? INT32_MAX : (int32_t)max_drain;
+  for (int32_t i = 0; i < ticks; ++i) {
+    hipLaunchKernelGGL(k_drain_ctl, dim3(1), dim3(1), 0, s, p, n_before, md);
+    hipLaunchKernelGGL(k_pick, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, kTimeFromDevice);
+    hipLaunchKernelGGL(k_marker, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, kTimeFromDevice);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
+    launch_push(p, kTimeFromDevice, s);
+  }
+  return hipGetLastError();
+}
+
+int cg_launch_drain_end(const GParams& p, void* stream) {
+  hipLaunchKernelGGL(k_drain_end, dim3(1), dim3(1), 0, (hipStream_t)stream, p);
   return hipGetLastError();
 }
 

@@ -885,6 +885,16 @@ static int drain_events(orc_sim* s, int num_snapshots, int64_t max_drain_ticks) 
     return ORC_OK;
 }
 
+/* The drain of readEventsFile (test_common.go:123-137) on its own, after a program run
+ * (orc_run_program): tick until every snapshot not yet collected has completed, then
+ * maxDelay+1 more ticks. */
+int orc_drain(orc_sim* s, int64_t max_drain_ticks) {
+    if (s->status) return s->status;
+    int pending = 0;
+    for (int sid = 0; sid < s->next_snapshot_id; sid++) pending += !s->collected[sid];
+    return drain_events(s, pending, max_drain_ticks);
+}
+
 int orc_read_events(orc_sim* s, const char* path, int64_t max_drain_ticks) {
     char* b = read_file(path, NULL);
     if (!b) return ORC_ERR_PARSE;

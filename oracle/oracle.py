@@ -69,6 +69,7 @@ def lib():
             "orc_traffic_sends": (C.c_int, [vp, C.c_uint64, C.c_uint32, i64]),
             "orc_run_program": (C.c_int, [vp, i64, C.c_uint64, C.c_uint32, i64, C.c_int, vp, vp]),
             "orc_collect_channels": (i64, [vp, C.c_int, vp, vp, vp, i64]),
+            "orc_drain": (C.c_int, [vp, i64]),
             "orc_num_links": (C.c_int, [vp]),
             "orc_queue_depths": (None, [vp, vp]),
             "orc_log_enable": (None, [vp, C.c_int]),
@@ -226,6 +227,10 @@ class OracleSim:
         sr = np.ascontiguousarray(snap_rank, dtype=np.int32)
         return self._L.orc_run_program(self._h, steps, traffic_seed, thresh, traffic_steps, ss.size,
                                        _ptr(ss), _ptr(sr))
+
+    def drain(self, max_drain=MAX_DRAIN_TICKS):
+        """readEventsFile's drain (test_common.go:123-137) after a program run."""
+        return self._L.orc_drain(self._h, max_drain)
 
     @property
     def num_links(self):

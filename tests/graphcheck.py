@@ -63,16 +63,58 @@ def _snaps(n, snaps, seed):
     return ss, sr
 
 
-def oracle_program(p):
+def oracle_program(p, drain=False, max_drain=10000):
     s = O.OracleSim()
     s.use_counter_hash(p.delay_seed)
     assert s.build_graph(p.tokens, p.src, p.dst, p.width()) == 0
-    s.run_program(p.steps, p.traffic_seed, p.thresh, p.traffic_steps, p.snap_step, p.snap_rank)
+    rc = s.run_program(p.steps, p.traffic_seed, p.thresh, p.traffic_steps, p.snap_step, p.snap_rank)
+    if drain and rc == 0:
+        s.drain(max_drain)
     return s
 
 
-def engine_program(p, device=0, run=True, lanes=0):
-    g = clg.GraphSim(device=device, fifo_slots=p.fifo_slots)
+def run_summary(status, time, counters, cticks, digests, tokens):
+    """A compact, exact summary of a finished run (golden fixtures of runs too slow for
+    the oracle inside a GPU test): everything compare() checks, with the per-snapshot
+    message lists and token maps folded into digest_from_oracle's content digest."""
+    return {"status": int(status), "time": int(time),
+            "counters": {k: int(counters[k]) for k in ("push", "peek", "pop_tok", "pop_mk", "recorded",
+                                                        "completed")},
+            "ctick": [int(x) for x in cticks], "digest": [int(x) for x in digests],
+            "final_tokens_sum": int(np.sum(tokens)),
+            "final_tokens_hash": int(np.uint64(G.mix64_np(np.asarray(tokens, dtype=np.uint64) ^
+                                                          np.arange(len(tokens), dtype=np.uint64))
+                                              .sum(dtype=np.uint64)).astype(np.int64))}
+
+
+def oracle_summary(o):
+    nt = o.node_tokens()
+    tok = np.array([nt[k] for k in o.node_ids()], dtype=np.int64)
+    sids = range(o.num_snapshots)
+    with np.errstate(over="ignore"):
+        return run_summary(o.status, o.time, o.counters(), [o.completion_tick(s) for s in sids],
+                           [digest_from_oracle(o, [s]) for s in sids], tok)
+
+
+def engine_summary(g):
+    """The same summary from the engine, computed on the device (per-sid digests: the
+    engine's CL_GSUM_DIGEST restated per snapshot from collect_arrays)."""
+    sids = range(g.num_snapshots)
+    digs = []
+    for s in sids:
+        if g.snapshot_tick(s) < 0:
+            digs.append(0)
+            continue
+        tok, off, vals = g.collect_arrays(s)
+        digs.append(digest_of(s, tok, off, vals))
+    with np.errstate(over="ignore"):
+        return run_summary(g.status(), g.time(), g.counters(), [g.snapshot_tick(s) for s in sids], digs,
+                           g.node_tokens_array())
+
+
+def engine_program(p, device=0, run=True, lanes=0, drain=False, max_drain=10000):
+    g = clg.GraphSim(device=device, fifo_slots=p.fifo_slots, max_snapshots=len(p.snap_step),
+                     max_drain_ticks=max_drain)
     g.set_push_lanes(lanes)
     g.set_topology(p.tokens, p.src, p.dst, id_width=p.width())
     g.set_delay_hash(p.delay_seed)
@@ -83,6 +125,8 @@ def engine_program(p, device=0, run=True, lanes=0):
             g.start_snapshot_rank(int(p.snap_rank[si]))
             si += 1
         g.Tick(1)
+    if drain:
+        g.drain()
     if run:
         g.flush()
     return g
@@ -116,21 +160,28 @@ def compare(g, o, check_counters=True):
 
 def digest_from_oracle(o, sids=None):
     """CL_GSUM_DIGEST restated over the oracle's completed snapshots."""
-    total = np.uint64(0)
+    total = 0
     for sid in range(o.num_snapshots) if sids is None else sids:
         if not o.complete(sid):
             continue
         tok, off, vals = o.collect_channels(sid)
-        n = tok.size
-        with np.errstate(over="ignore"):
-            h = G.counter_hash_np(0x5107, np.full(n, sid, dtype=np.uint64), np.arange(n, dtype=np.uint64))
-            total += G.mix64_np(h ^ tok.astype(np.uint32).astype(np.uint64)).sum(dtype=np.uint64)
-            cnt = np.diff(off).astype(np.uint64)
-            cs = np.concatenate([[0], np.cumsum(vals, dtype=np.int64)])
-            sums = (cs[off[1:]] - cs[off[:-1]]).astype(np.uint32).astype(np.uint64)
-            e = cnt.size
-            hc = G.counter_hash_np(0xC4A1, np.full(e, sid, dtype=np.uint64), np.arange(e, dtype=np.uint64))
-            total += G.mix64_np(hc ^ ((cnt << np.uint64(32)) | sums)).sum(dtype=np.uint64)
+        total += digest_of(sid, tok, off, vals)
+    return int(np.uint64(total % (1 << 64)).astype(np.int64))
+
+
+def digest_of(sid, tok, off, vals):
+    """The content digest of one snapshot (tokens by rank, channel CSR of payloads), as
+    an int64 -- the per-snapshot term of CL_GSUM_DIGEST (cg_kernels.hip k_checks_snap)."""
+    n = tok.size
+    with np.errstate(over="ignore"):
+        h = G.counter_hash_np(0x5107, np.full(n, sid, dtype=np.uint64), np.arange(n, dtype=np.uint64))
+        total = G.mix64_np(h ^ tok.astype(np.uint32).astype(np.uint64)).sum(dtype=np.uint64)
+        cnt = np.diff(off).astype(np.uint64)
+        cs = np.concatenate([[0], np.cumsum(vals, dtype=np.int64)])
+        sums = (cs[off[1:]] - cs[off[:-1]]).astype(np.uint32).astype(np.uint64)
+        e = cnt.size
+        hc = G.counter_hash_np(0xC4A1, np.full(e, sid, dtype=np.uint64), np.arange(e, dtype=np.uint64))
+        total += G.mix64_np(hc ^ ((cnt << np.uint64(32)) | sums)).sum(dtype=np.uint64)
     return int(total.astype(np.int64))
 
 

@@ -16,7 +16,7 @@ import pytest
 
 import graphgen as G
 import oracle as O
-from graphcheck import (clg, cl, compare, digest_from_oracle, engine_program, oracle_program,
+from graphcheck import (clg, cl, compare, digest_from_oracle, engine_program, engine_summary, oracle_program,
                         powerlaw_program, regular_program, scenario_engine, scenario_oracle, Program)
 from snapcheck import assert_equal, check_tokens, read_snapshot_file, scenarios
 
@@ -314,13 +314,49 @@ def test_c4_full_size_properties():
     assert g.checksums() == sums
 
 
+@pytest.mark.parametrize("lanes", [1, 8])
+def test_powerlaw_with_drain_vs_oracle(lanes):
+    """C5-shaped run followed by readEventsFile's drain (test_common.go:123-137, on the
+    device: k_drain_ctl before every tick): every snapshot completes, bit-exact."""
+    p = powerlaw_program(2000, 60, 32, fifo_slots=512)
+    g = engine_program(p, lanes=lanes, drain=True)
+    o = oracle_program(p, drain=True)
+    assert o.status == 0 and all(o.complete(s) for s in range(32))
+    compare(g, o)
+    assert g.checksums()["digest"] == digest_from_oracle(o)
+    g.rerun()
+    g.synchronize()
+    compare(g, o)
+
+
+def test_c5_shape_20k_nodes_256_snapshots_vs_oracle_fixture():
+    """The largest C5-shaped run the CPU oracle finishes in minutes (20,000 nodes, one
+    snapshot start per tick for 256 ticks under traffic, then the drain until all 256
+    complete: ~52M delivered packets): the engine's exact run summary equals the
+    oracle's (tests/golden/graph_runs.json, tools/gen_graph_fixture.py)."""
+    import json
+    from snapcheck import ROOT
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "graph_runs.json")))["runs"]["c5_shape_20k_256"]
+    p = powerlaw_program(fx["nodes"], fx["steps"], fx["snapshots"], fifo_slots=fx["fifo_slots"])
+    g = engine_program(p, drain=True, max_drain=fx["max_drain"])
+    want = fx["summary"]
+    got = engine_summary(g)
+    assert got["status"] == 0 and all(t >= 0 for t in got["ctick"])
+    for k in want:
+        assert got[k] == want[k], k
+    sums = g.checksums()
+    assert sums["completed"] == fx["snapshots"] and sums["cut_residual"] == 0 and sums["final_residual"] == 0
+
+
 def test_c5_full_size_properties():
     """BASELINE config 5 at full size: 100k-node power-law digraph (8 Zipf(0.9) targets
-    + ring), one snapshot start per tick for 4,096 ticks under continuous traffic,
-    4,100 ticks.  Head-of-line scanning in dest order (sim.go:76-90) starves a busy
-    sender's higher links, so channels hold up to all 4,096 markers (8,192 slots)."""
+    + ring), one snapshot start per tick for 4,096 ticks under continuous traffic for
+    4,100 ticks, then readEventsFile's drain until all 4,096 snapshots complete (+6).
+    Head-of-line scanning in dest order (sim.go:76-90) serializes each sender's marker
+    fan-out, so channels hold up to all 4,096 markers (8,192 slots) and the drain runs
+    for tens of thousands of ticks."""
     n, steps, snaps = 100_000, 4100, 4096
-    g = clg.GraphSim(fifo_slots=8192, max_snapshots=snaps)
+    g = clg.GraphSim(fifo_slots=8192, max_snapshots=snaps, max_drain_ticks=200_000)
     g.generate_powerlaw(n, 8, 0.9, True, 100, seed=30240)
     g.set_delay_hash(30241)
     g.set_traffic(30242, 1 << 30, steps)
@@ -328,12 +364,14 @@ def test_c5_full_size_properties():
         if 1 <= k <= snaps:
             g.start_snapshot_rank(G.mulhi(G.counter_hash(30243, k - 1, 1), n))
         g.Tick(1)
+    g.drain()
     g.flush()
     assert g.status() == 0
     sums = g.checksums()
+    assert sums["completed"] == snaps
     assert sums["final_residual"] == 0 and sums["cut_residual"] == 0
     c = g.counters()
-    assert c["pop_mk"] <= snaps * g.num_channels
+    assert c["pop_mk"] == snaps * g.num_channels       # every marker of every snapshot delivered
     assert c["pop_tok"] + c["pop_mk"] == sums["delivered"]
     assert c["push"] >= sums["delivered"]
     g.rerun()

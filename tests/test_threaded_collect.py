@@ -77,10 +77,16 @@ def read_events_file(sim, text):
     return snapshots
 
 
+@pytest.mark.parametrize("delays", ["go_seed", "predrawn_schedule"])
 @pytest.mark.parametrize("sc", scenarios(), ids=lambda s: s["name"])
-def test_run_test_with_collector_threads(sc):
-    """runTest (snapshot_test.go:11-44) with blocking collector threads."""
+def test_run_test_with_collector_threads(sc, delays):
+    """runTest (snapshot_test.go:11-44) with blocking collector threads.  Delays come
+    from the engine's Go stream for rand.Seed(seed + 1), or -- as the cgo shim in
+    INTEGRATION.md does -- from that stream pre-drawn on the host and passed as an
+    explicit schedule."""
     sim = cl.ChandyLamportSim(1, seed_base=O.REFERENCE_SEED)   # rand.Seed(seed + 1)
+    if delays == "predrawn_schedule":
+        sim.set_delay_schedule(cl.go_delay_schedule(O.REFERENCE_SEED, 1, 1 << 16))
     sim.read_topology_text(read_text(sc["top"]))
     snaps = read_events_file(sim, read_text(sc["events"]))
     assert sim.status()[0] == cl.INST_OK
