@@ -638,24 +638,35 @@ struct cl_sim {
   }
 
   // Instances of [lo, hi) in which snapshot sid has completed, as of every event issued
-  // so far (pending events are executed; no tick is added).
-  int count_complete(int32_t sid, int64_t lo, int64_t hi, int64_t* n) {
+  // so far (pending events are executed; no tick is added), and how many of the others
+  // are frozen (a FATAL / HANG / engine-limit status: their snapshot can never complete).
+  int count_complete(int32_t sid, int64_t lo, int64_t hi, int64_t* n, int64_t* n_frozen = nullptr) {
     int rc = flush();
     if (rc) return rc;
-    const int32_t* t;
-    std::vector<int32_t> plane;
+    const int32_t *t, *st;
+    std::vector<int32_t> plane, stat;
     if (h_valid) {
       t = h_snap_tick.data() + (size_t)sid * stride + lo;
+      st = h_regs.data() + (size_t)R_STATUS * stride + lo;
     } else {
       plane.resize((size_t)(hi - lo));
-      if (hi > lo)
+      stat.resize((size_t)(hi - lo));
+      if (hi > lo) {
         HIP_TRY(hipMemcpy(plane.data(), d_snap_tick.p + (size_t)sid * stride + lo, plane.size() * sizeof(int32_t),
                           hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(stat.data(), d_regs.p + (size_t)R_STATUS * stride + lo, stat.size() * sizeof(int32_t),
+                          hipMemcpyDeviceToHost));
+      }
       t = plane.data();
+      st = stat.data();
     }
-    int64_t c = 0;
-    for (int64_t i = 0; i < hi - lo; ++i) c += t[i] >= 0;
+    int64_t c = 0, f = 0;
+    for (int64_t i = 0; i < hi - lo; ++i) {
+      c += t[i] >= 0;
+      f += t[i] < 0 && st[i] != ST_OK;
+    }
     *n = c;
+    if (n_frozen) *n_frozen = f;
     return CL_OK;
   }
 
@@ -1120,11 +1131,14 @@ int cl_wait_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi,
     return set_err(CL_E_INVALID, "snapshot/instance range out of range");
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
   for (;;) {
-    int64_t n = 0;
-    int rc = sim->count_complete(sid, inst_lo, inst_hi, &n);
+    int64_t n = 0, frozen = 0;
+    int rc = sim->count_complete(sid, inst_lo, inst_hi, &n, &frozen);
     if (rc) return rc;
     if (n_complete) *n_complete = n;
     if (n == inst_hi - inst_lo) return CL_OK;
+    if (n + frozen == inst_hi - inst_lo)  // the rest stopped at a fatal: they never complete
+      return set_err(CL_E_NOT_COMPLETE, "snapshot %d: %lld of %lld instances complete, %lld stopped (status != ok)",
+                     sid, (long long)n, (long long)(inst_hi - inst_lo), (long long)frozen);
     const uint64_t gen = sim->exec_gen;
     auto more = [&] { return sim->exec_gen != gen; };
     if (timeout_ms < 0) {

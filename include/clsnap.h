@@ -178,7 +178,10 @@ int cl_poll_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi,
  * completed in every instance of [inst_lo, inst_hi).  The caller is a collector thread;
  * it is woken after each execution of the driver's events (cl_flush, queries) and
  * re-checks.  timeout_ms < 0 waits forever; on timeout returns CL_E_NOT_COMPLETE with
- * *n_complete (may be NULL) set.  Never ticks. */
+ * *n_complete (may be NULL) set.  It also returns CL_E_NOT_COMPLETE at once when every
+ * instance of the range has either completed or stopped with a non-OK status (the
+ * reference process would have exited at that log.Fatal; such an instance never
+ * completes).  Never ticks. */
 int cl_wait_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t timeout_ms,
                      int64_t* n_complete);
 /* CollectSnapshot (sim.go:134-173) of instances [inst_lo, inst_hi) at once:

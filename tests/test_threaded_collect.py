@@ -13,6 +13,7 @@ import importlib
 import queue
 import threading
 
+import numpy as np
 import pytest
 
 import oracle as O
@@ -115,6 +116,12 @@ def test_poll_wait_and_range_collect_over_a_batch():
             results["waited"] = sim.wait_snapshot(0, 0, 64, timeout_ms=COLLECT_TIMEOUT_MS)
         except Exception as e:
             results["error"] = e
+
+    def waiter_all():   # includes instances that stop at a fatal: returns, does not hang
+        try:
+            results["all"] = sim.wait_snapshot(0, 0, n, timeout_ms=COLLECT_TIMEOUT_MS)
+        except cl.ClSnapError as e:
+            results["all_error"] = e
     started = False
     th = None
     for line in lines:
@@ -127,6 +134,8 @@ def test_poll_wait_and_range_collect_over_a_batch():
                 sim.flush()
                 th = threading.Thread(target=waiter, daemon=True)
                 th.start()
+                th2 = threading.Thread(target=waiter_all, daemon=True)
+                th2.start()
                 started = True
         else:
             for _ in range(int(f[1]) if len(f) > 1 else 1):
@@ -135,10 +144,16 @@ def test_poll_wait_and_range_collect_over_a_batch():
     sim.drain()
     sim.flush()
     th.join(timeout=30)
-    assert "error" not in results and results["waited"] == 64
+    th2.join(timeout=30)
+    status = sim.status()
+    if (status[:64] == cl.INST_OK).all():
+        assert "error" not in results and results["waited"] == 64
+    else:    # a fatal instance in the range: the waiter returns NOT_COMPLETE instead of hanging
+        assert results["error"].code == -9
+    assert results["all_error"].code == -9 and (status != cl.INST_OK).any()
     ticks0 = sim_ticks(sim, 0)
     assert sim.poll_snapshot(0) == int((ticks0 >= 0).sum()) > 0.9 * n
-    assert sim.poll_snapshot(0, 0, 64) == 64
+    assert sim.poll_snapshot(0, 0, 64) == int((ticks0[:64] >= 0).sum())
     tok, done, off, msg = sim.collect_snapshot_range(4, 100, 164)
     ch = sim.num_channels
     for r, i in enumerate(range(100, 164)):
