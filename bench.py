@@ -333,7 +333,7 @@ def bench_graph(args, rank, world, local_rank):
     if os.path.exists(tr_path):
         with open(tr_path) as f:
             tr = json.load(f)
-        if tr.get("nodes") == n and tr.get("steps") == steps:
+        if tr.get("nodes") == n and tr.get("steps") == steps and tr.get("drain", False) == bool(cfg.get("drain")):
             traffic = tr.get("hbm_bytes_per_launch")
 
     if rank == 0:

@@ -138,11 +138,7 @@ struct Lane {
 #ifndef CLSNAP_MAX_D
 #define CLSNAP_MAX_D 128
 #endif
-//   CLSNAP_B_ROUNDS    phase B as rounds over the in-links that actually delivered (1): one
-//                      copy of the token/marker path per round instead of one per in-link
-#ifndef CLSNAP_B_ROUNDS
-#define CLSNAP_B_ROUNDS 0
-#endif
+
 constexpr bool unrolled(int D) { return D <= CLSNAP_UNROLL_MAX; }
 template <int D>
 using InLinks = uint32_t[unrolled(D) ? D : 1];
@@ -366,41 +362,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
   wave_sync();
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
-  if constexpr (CLSNAP_B_ROUNDS && D <= 32) {
-    // deliveries addressed to this receiver: one bit per in-link (in-link order is the
-    // reference's sender order, sim.go:76-90); then one round per delivery of the
-    // busiest receiver, every receiver handling its next delivery in that order
-    uint32_t dm = 0;
-    if (act) {
-#pragma unroll
-      for (int32_t ki = 0; ki < (unrolled(D) ? D : x.indeg); ++ki) {
-        if (ki >= x.indeg) break;
-        const uint32_t w = in_word<D>(x, it, ki);
-        const uint32_t pk = XW(lay.x_pick + x.seg_base + (w & 0xffu));
-        dm |= ((pk & kPickValid) && ((pk >> 16) & 0x7fu) == ((w >> 8) & 0xffu)) ? 1u << ki : 0u;
-      }
-    }
-    while (__ballot(dm != 0)) {
-      if (dm) {
-        const int32_t ki = __builtin_ctz(dm);
-        dm &= dm - 1;
-        const uint32_t w = PW(lay.w_int + ki);
-        const uint32_t src = w & 0xffu;
-        const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
-        const uint32_t pay = pk & 0xffffu;
-        temit<TRACE>(x, (pk & kMarkerBit) ? TK_RECV_MARKER : TK_RECV_TOKEN, src, ln.time, src << 8, (int32_t)pay,
-                     ln.tokens);
-        if (!(pk & kMarkerBit)) {  // HandleToken: tokens += data; the recording cursor advances
-          ln.pop_tok++;
-          ln.tokens += (int32_t)pay;
-          PW(lay.w_cur + ki) += 1u;
-        } else {
-          ln.pop_mk++;
-          handle_marker<D, TRACE>(x, ln, it, ki, w, src, (int32_t)pay, ntrig);
-        }
-      }
-    }
-  } else if constexpr (unrolled(D) && CLSNAP_B_PRED) {
+  if constexpr (unrolled(D) && CLSNAP_B_PRED) {
 #pragma unroll
     for (int32_t ki = 0; ki < D; ++ki) {
       if (ki >= lay.id) break;  // uniform: the layout holds id in-links per lane
@@ -656,7 +618,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
       XW(lay.x_ndone + seg) = Dn[lay.s_cap * st];
     }
   }
-  if constexpr (!unrolled(D) || CLSNAP_B_ROUNDS)
+  if constexpr (!unrolled(D))
     for (int32_t k = 0; k < indeg; ++k) PW(lay.w_int + k) = nb[3 + k];
   wave_sync();
   ln.alive = valid && ln.status == ST_OK;
