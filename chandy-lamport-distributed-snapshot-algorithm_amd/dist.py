@@ -25,3 +25,39 @@ def reduce_results(elapsed_s, sums, device):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
     return float(t.item()), [int(v) for v in s.tolist()]
+
+
+# ---- exchange layer of the graph-partitioned mode ---------------------
+# One simulation whose nodes are split into rank ranges exchanges, every tick, records
+# addressed to the owners of other nodes (deliveries, broadcast-trigger reports, draw
+# bases).  Records are fixed-width int64 rows; one all-to-all of counts sizes one
+# all-to-all of the rows (RCCL over xGMI for device tensors, gloo for host tensors).
+
+def exchange_rows(rows_by_dest, width, device="cpu"):
+    """rows_by_dest[r]: int64 array [k_r, width] for rank r.  Returns the list of the
+    arrays every rank addressed to this one, in source-rank order."""
+    world = dist.get_world_size()
+    counts = torch.tensor([len(r) for r in rows_by_dest], dtype=torch.int64, device=device)
+    recv_counts = torch.empty_like(counts)
+    dist.all_to_all_single(recv_counts, counts)
+    send = torch.cat([torch.as_tensor(r, dtype=torch.int64).reshape(-1, width) for r in rows_by_dest]).to(device) \
+        if any(len(r) for r in rows_by_dest) else torch.zeros((0, width), dtype=torch.int64, device=device)
+    rc = recv_counts.tolist()
+    recv = torch.empty((sum(rc), width), dtype=torch.int64, device=device)
+    dist.all_to_all_single(recv.view(-1), send.reshape(-1).contiguous(),
+                           output_split_sizes=[c * width for c in rc],
+                           input_split_sizes=[len(r) * width for r in rows_by_dest])
+    out, o = [], 0
+    host = recv.cpu().numpy()
+    for c in rc:
+        out.append(host[o:o + c])
+        o += c
+    return out
+
+
+def allgather_ints(values, device="cpu"):
+    """[world, len(values)] int64: every rank's values."""
+    t = torch.tensor([int(v) for v in values], dtype=torch.int64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return torch.stack(out).cpu().numpy()

@@ -1,6 +1,6 @@
 """HBM bytes per graph-engine run from the gpu_pmc_graph.sh passes -> profiles/traffic_<cfg>.json.
 
-usage: python tools/graph_traffic.py <cfg> <nodes> <ticks>
+usage: python tools/graph_traffic.py <cfg> <nodes> <ticks> [drain]
 A run is k_reset + the tick kernels (k_hostops, k_tally, k_pick, k_marker, k_scan, k_push);
 the post-run checks (k_finish, k_checks_*) are excluded.  Runs = k_reset dispatches.
 Bytes follow MI355X_MICROARCH.md's gfx950 correction as tools/make_profiles.py does:
@@ -14,33 +14,40 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RUN_KERNELS = {"k_reset", "k_hostops", "k_tally", "k_pick", "k_marker", "k_scan", "k_push"}
+RUN_KERNELS = {"k_reset", "k_hostops", "k_tally", "k_pick", "k_marker", "k_scan", "k_push",
+               "k_drain_begin", "k_drain_ctl", "k_drain_end"}
 
 
 def sums(pattern):
     tot = collections.Counter()
+    per_kernel = collections.Counter()
     resets = set()
     for p in glob.glob(pattern, recursive=True):
         for r in csv.DictReader(open(p)):
-            m = re.search(r"(k_\w+)\(", r["Kernel_Name"])
+            m = re.search(r"(k_\w+)", r["Kernel_Name"])
             if not m or m.group(1) not in RUN_KERNELS:
                 continue
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
+            per_kernel[m.group(1)] += float(r["Counter_Value"])
             if m.group(1) == "k_reset":
                 resets.add(r["Dispatch_Id"])
-    return tot, len(resets)
+    return tot, len(resets), per_kernel
 
 
 cfg, nodes, ticks = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 base = os.path.join(ROOT, "gpurun_out", f"pmcg_{cfg}")
-f, runs_f = sums(os.path.join(base, "pass3", "**", "*counter_collection.csv"))
-w, runs_w = sums(os.path.join(base, "pass4", "**", "*counter_collection.csv"))
+drain = len(sys.argv) > 4 and sys.argv[4] == "drain"
+f, runs_f, fk = sums(os.path.join(base, "pass3", "**", "*counter_collection.csv"))
+w, runs_w, wk = sums(os.path.join(base, "pass4", "**", "*counter_collection.csv"))
 assert runs_f and runs_w, "no k_reset dispatches found"
 fetch_kb = f["FETCH_SIZE"] / runs_f
 write_kb = w["WRITE_SIZE"] / runs_w
-out = {"config": cfg, "nodes": nodes, "steps": ticks, "runs_profiled": runs_f,
+out = {"config": cfg, "nodes": nodes, "steps": ticks, "drain": drain, "runs_profiled": runs_f,
        "fetch_kb_per_run": fetch_kb, "write_kb_per_run": write_kb,
        "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
+       "per_kernel_bytes_per_run": {k: (2 * fk[k] / runs_f + wk[k] / runs_w) * 1024 for k in sorted(fk)},
+       "per_kernel_fetch_kb_per_run": {k: fk[k] / runs_f for k in sorted(fk)},
+       "per_kernel_write_kb_per_run": {k: wk[k] / runs_w for k in sorted(wk)},
        "note": "one launch = one full run of the tick pipeline; (2*FETCH_SIZE + WRITE_SIZE) KB per gfx950 correction"}
 json.dump(out, open(os.path.join(ROOT, "profiles", f"traffic_{cfg}.json"), "w"), indent=1)
 print(json.dumps(out))
