@@ -119,6 +119,32 @@ def lib():
 LOG_SENT_TOKEN, LOG_SENT_MARKER, LOG_RECV_TOKEN, LOG_RECV_MARKER, LOG_START, LOG_END = range(6)
 
 
+def format_log(ids, records):
+    """Logger.PrettyPrint (logger.go:55-64) of (epoch, kind, node, other, data, tokens)
+    records: LogEvent.String / the record String methods (logger.go:25-50,
+    common.go:75-122)."""
+    name = lambda r: ids[r] if r >= 0 else "?"  # noqa: E731  (no link: the dest string is not kept)
+    lines, epoch = [], None
+    for ep, kind, node, other, data, tokens in records:
+        if ep != epoch:
+            lines.append(f"Time {ep}:")
+            epoch = ep
+        if kind == LOG_SENT_TOKEN:
+            rec, pre = f"{ids[node]} sent {data} tokens to {name(other)}", True
+        elif kind == LOG_SENT_MARKER:
+            rec, pre = f"{ids[node]} sent marker({data}) to {name(other)}", False
+        elif kind == LOG_RECV_TOKEN:
+            rec, pre = f"{ids[node]} received {data} tokens from {name(other)}", True
+        elif kind == LOG_RECV_MARKER:
+            rec, pre = f"{ids[node]} received marker({data}) from {name(other)}", False
+        elif kind == LOG_START:
+            rec, pre = f"{ids[node]} startSnapshot({data})", True
+        else:
+            rec, pre = f"{ids[node]} endSnapshot({data})", False
+        lines.append(f"\t{ids[node]} has {tokens} token(s)\n\t{rec}" if pre else f"\t{rec}")
+    return "\n".join(lines) + ("\n" if lines else "")
+
+
 def _check(rc):
     if rc != 0:
         raise ClSnapError(rc, lib().cl_last_error().decode())
@@ -436,27 +462,7 @@ class ChandyLamportSim:
 
     def pretty_print(self, instance=0):
         """Logger.PrettyPrint (logger.go:55-64) of a traced instance, as text."""
-        ids = self.node_ids()
-        name = lambda r: ids[r] if r >= 0 else "?"  # noqa: E731  (no link: the dest string is not kept)
-        lines, epoch = [], None
-        for ep, kind, node, other, data, tokens in self.trace(instance):
-            if ep != epoch:
-                lines.append(f"Time {ep}:")
-                epoch = ep
-            if kind == LOG_SENT_TOKEN:   # LogEvent.String / SentMsgRecord.String (logger.go:25-50, common.go:81-87)
-                rec, pre = f"{ids[node]} sent {data} tokens to {name(other)}", True
-            elif kind == LOG_SENT_MARKER:
-                rec, pre = f"{ids[node]} sent marker({data}) to {name(other)}", False
-            elif kind == LOG_RECV_TOKEN:  # ReceivedMsgRecord.String (common.go:116-122)
-                rec, pre = f"{ids[node]} received {data} tokens from {name(other)}", True
-            elif kind == LOG_RECV_MARKER:
-                rec, pre = f"{ids[node]} received marker({data}) from {name(other)}", False
-            elif kind == LOG_START:       # common.go:95-97
-                rec, pre = f"{ids[node]} startSnapshot({data})", True
-            else:                         # common.go:105-107
-                rec, pre = f"{ids[node]} endSnapshot({data})", False
-            lines.append(f"\t{ids[node]} has {tokens} token(s)\n\t{rec}" if pre else f"\t{rec}")
-        return "\n".join(lines) + ("\n" if lines else "")
+        return format_log(self.node_ids(), self.trace(instance))
 
     @staticmethod
     def status_string(code):

@@ -73,6 +73,23 @@ struct ChIn {
 
 constexpr uint32_t kEmpty = 0xffffffffu;  // head receiveTime word of an empty channel
 
+// Device event trace of the graph engine (the reference's debug Logger, logger.go:12-76).
+// One record per LogEvent, appended unordered; the host sorts them into the Logger's order
+// by (epoch, order, sub) and restores LogEvent.nodeTokens by replaying the token changes the
+// records themselves carry (cg_host.cpp cl_graph_trace_read).  Within an epoch (= simulator
+// time, Logger.NewEpoch per Tick, sim.go:73) the Logger holds the tick's deliveries in
+// sender rank order (sim.go:76-90), then the traffic sends of that step in node order, then
+// the host events in program order.
+enum : uint32_t { kTrTick = 0u, kTrSend = 1u, kTrHost = 2u };
+constexpr uint32_t kTrSubEnd = 0xffffffffu;  // EndSnapshotRecord after the delivery's records
+struct GTraceRec {
+  int32_t epoch;
+  uint32_t order;  // part (bits 31..30) | key: sender rank (tick), node rank (send), op index (host)
+  uint32_t sub;    // 0 the delivery / send / start record, 1 + j the broadcast on out-link j, kTrSubEnd
+  int32_t kind;    // TK_* (cl_engine.h) == CL_LOG_* (clsnap.h)
+  int32_t node, other, data, pad;
+};
+
 enum GOpKind : int32_t { GOP_SEND = 1, GOP_SNAP = 2 };
 struct GOp {
   int32_t kind, a, b;  // SEND: a = src rank, b = dest rank; SNAP: a = node rank, b = snapshot id
@@ -145,6 +162,11 @@ struct GParams {
   int32_t* ctick;      // [s_cap] completion tick (-1)
   GScal* sc;
   const GOp* ops;
+  // event trace (nullptr: off)
+  GTraceRec* trace;
+  uint32_t* trace_cnt;
+  int32_t trace_cap;
+  int32_t pad1;
 };
 
 // Launchers (cg_kernels.hip); return hipError_t as int.

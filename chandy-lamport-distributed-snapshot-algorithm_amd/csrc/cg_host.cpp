@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <tuple>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -170,6 +172,10 @@ struct cl_graph {
   GBuf<uint8_t> d_sched;
   GBuf<unsigned long long> d_scratch;
   size_t ops_uploaded = 0;
+  // device event trace (cl_graph_trace_enable)
+  int32_t trace_cap = 0;
+  GBuf<GTraceRec> d_trace;
+  GBuf<uint32_t> d_trace_cnt;
 
   ~cl_graph() {
     if (!dev_ready) return;
@@ -182,6 +188,7 @@ struct cl_graph {
     d_cre.release(); d_bsum.release(); d_hq.release(); d_histv.release(); d_mlist.release(); d_route.release();
     d_chin.release(); d_fifo.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
     d_sched.release(); d_scratch.release(); d_big.release(); d_cpart.release();
+    d_trace.release(); d_trace_cnt.release();
     for (auto& ev : ev_pool) {
       (void)hipEventDestroy(ev.first);
       (void)hipEventDestroy(ev.second);
@@ -471,6 +478,9 @@ struct cl_graph {
     p.ctick = d_ctick.p;
     p.sc = d_sc.p;
     p.ops = d_ops.p;
+    p.trace = trace_cap > 0 ? d_trace.p : nullptr;
+    p.trace_cnt = trace_cap > 0 ? d_trace_cnt.p : nullptr;
+    p.trace_cap = trace_cap;
   }
 
   int upload_ops() {
@@ -546,6 +556,7 @@ struct cl_graph {
     bool realloc = false;
     if ((rc = ensure_state(&realloc))) return rc;
     if ((rc = ensure_sched()) || (rc = upload_ops())) return rc;
+    if (trace_cap > 0 && ((rc = d_trace.ensure((size_t)trace_cap)) || (rc = d_trace_cnt.ensure(1)))) return rc;
     fill_params();
     if (realloc || !state_valid) fresh = true;
     if (!fresh && executed == prog.size()) return CL_OK;
@@ -564,6 +575,8 @@ struct cl_graph {
       time = 0;
       hang = false;
       if ((rc = k_err(cg_launch_reset(P, d_init_tok.p, stream)))) return rc;
+      // a replay from the initial state restarts the log (an incremental run appends)
+      if (trace_cap > 0) GHIP(hipMemsetAsync(d_trace_cnt.p, 0, sizeof(uint32_t), stream));
       if (traffic_steps > 0 && (rc = k_err(cg_launch_sends(P, 0, stream)))) return rc;  // step 0 traffic
     }
     state_valid = false;
@@ -1115,6 +1128,61 @@ int cl_graph_collect_snapshot(cl_graph* g, int32_t sid, int64_t* tokens, int64_t
     const uint32_t b = (uint32_t)x, e = (uint32_t)(x >> 32);
     for (uint32_t q = b; q < e; ++q)
       msg_tokens[msg_offsets[c] + (q - b)] = g->hist ? (int64_t)hv[k * g->hist + q] : 1;
+  }
+  return CL_OK;
+}
+
+int cl_graph_trace_enable(cl_graph* g, int32_t capacity) {
+  G_CHECK(g);
+  if (capacity < 0) return gerr(CL_E_INVALID, "negative trace capacity");
+  g->trace_cap = capacity;
+  g->state_valid = false;  // the next flush replays the program with tracing on (or off)
+  return CL_OK;
+}
+
+int cl_graph_trace_read(cl_graph* g, cl_log_event* out, int32_t cap, int32_t* n_events) {
+  G_CHECK(g);
+  if (!n_events) return gerr(CL_E_INVALID, "null output");
+  if (g->trace_cap <= 0) return gerr(CL_E_INVALID, "tracing is off (cl_graph_trace_enable)");
+  int rc = g->flush();
+  if (rc) return rc;
+  uint32_t cnt = 0;
+  GHIP(hipMemcpy(&cnt, g->d_trace_cnt.p, sizeof cnt, hipMemcpyDeviceToHost));
+  const uint32_t have = std::min<uint32_t>(cnt, (uint32_t)g->trace_cap);
+  std::vector<GTraceRec> r(have);
+  if (have) GHIP(hipMemcpy(r.data(), g->d_trace.p, have * sizeof(GTraceRec), hipMemcpyDeviceToHost));
+  if (cnt > (uint32_t)g->trace_cap)
+    return gerr(CL_E_LIMIT, "trace overflowed: %u records, capacity %d", cnt, g->trace_cap);
+  // EndSnapshotRecord (sim.go:127) follows the delivery that completed the local snapshot:
+  // the last marker of that snapshot delivered to the node in that tick, in sender order
+  // (the device counts completions in whatever order the atomics land).
+  std::map<std::tuple<int32_t, int32_t, int32_t>, uint32_t> last;
+  for (const auto& x : r)
+    if (x.kind == TK_RECV_MARKER && (x.order >> 30) == kTrTick) {
+      auto& l = last[std::make_tuple(x.epoch, x.node, x.data)];
+      l = std::max(l, x.order & 0x3fffffffu);
+    }
+  for (auto& x : r)
+    if (x.kind == TK_END) x.order = (kTrTick << 30) | last[std::make_tuple(x.epoch, x.node, x.data)];
+  std::sort(r.begin(), r.end(), [](const GTraceRec& a, const GTraceRec& b) {
+    return std::make_tuple(a.epoch, a.order, a.sub) < std::make_tuple(b.epoch, b.order, b.sub);
+  });
+  // LogEvent.nodeTokens (logger.go:71-76): the node's tokens when the record is made --
+  // replayed from the initial tokens through the token changes the records carry
+  std::vector<int64_t> tok(g->init_tok.begin(), g->init_tok.end());
+  *n_events = (int32_t)have;
+  for (uint32_t i = 0; i < have; ++i) {
+    const GTraceRec& x = r[i];
+    if (out && (int32_t)i < cap) {
+      out[i].epoch = x.epoch;
+      out[i].kind = x.kind;
+      out[i].node = x.node;
+      out[i].other = x.other;
+      out[i].data = x.data;
+      out[i].tokens = (int32_t)tok[x.node];
+    }
+    if (x.kind == TK_SENT_TOKEN) tok[x.node] -= x.data;       // node.go:118-120
+    else if (x.kind == TK_RECV_TOKEN) tok[x.node] += x.data;  // node.go:175
   }
   return CL_OK;
 }

@@ -82,6 +82,16 @@ __device__ inline bool block_frozen(const GParams& p) {
 
 __device__ inline void set_status(GScal* sc, int32_t code) { atomicCAS(&sc->status, 0, code); }
 
+// Append one Logger record (trace runs only; one device counter: a debugging aid for
+// graphs of modest size).
+__device__ inline void gtrace(const GParams& p, int32_t epoch, uint32_t part, uint32_t key, uint32_t sub, int32_t kind,
+                              int32_t node, int32_t other, int32_t data) {
+  if (!p.trace) return;
+  const uint32_t slot = atomicAdd(p.trace_cnt, 1u);
+  if (slot < (uint32_t)p.trace_cap)
+    p.trace[slot] = GTraceRec{epoch, (part << 30) | (key & 0x3fffffffu), sub, kind, node, other, data, 0};
+}
+
 // GetReceiveTime (sim.go:100-102) for draw index k at simulator time `time`.
 __device__ inline uint32_t receive_time(const GParams& p, uint64_t k, int32_t time) {
   uint32_t d;
@@ -361,6 +371,9 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
       ChIn* ci = &p.chin[k];
       ci->tick = (uint32_t)t;
       ci->pay = pay;
+      // ReceivedMsgRecord (sim.go:86)
+      gtrace(p, t, kTrTick, (uint32_t)s, 0u, (pay & kGMarker) ? TK_RECV_MARKER : TK_RECV_TOKEN, v, s,
+             (int32_t)(pay & kGPayload));
       if (pay & kGMarker) {
         const int32_t sid = (int32_t)(pay & kGPayload);
         atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + v], ((unsigned long long)t << 32) | (uint32_t)s);
@@ -423,6 +436,9 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
     if (key == (((uint64_t)t << 32) | (uint32_t)s0)) {
       // first marker: CreateLocalSnapshot(src) + SendToNeighbors (node.go:153-156)
       s_trig[s0 - blockIdx.x * kGThreads] = p.out_off[v + 1] - p.out_off[v];
+      if (p.trace)  // SendToNeighbors' SentMsgRecords (node.go:100)
+        for (int32_t j = p.out_off[v]; j < p.out_off[v + 1]; ++j)
+          gtrace(p, t, kTrTick, (uint32_t)s0, 1u + (uint32_t)(j - p.out_off[v]), TK_SENT_MARKER, v, p.route[j].x, sid);
       const int slot = atomicAdd(&p.crn[v], 1);
       p.cre[lo + slot] = ((uint64_t)(uint32_t)s0 << 32) | (uint32_t)sid;
       bx = BigX{lo, hi, s0, sid, k, v, {0, 0}};
@@ -444,6 +460,10 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
       }  // else created this tick by a lower-ranked sender: its expansion closes it
       done = atomicAdd(&p.cnt[sv], -1) - 1 == kBig;
     }
+  }
+  if (done && p.trace) {  // EndSnapshotRecord (sim.go:127); the host moves it behind the last marker
+    const MDel m = p.mlist[blockIdx.x * kGThreads + threadIdx.x];
+    gtrace(p, t, kTrTick, (uint32_t)m.s0, kTrSubEnd, TK_END, vdone, -1, sid);
   }
   complete_nodes(p, done, sid, vdone, t, c[1]);
   const int idx[2] = {GC_RECORDED, GC_COMPLETED};
@@ -603,7 +623,10 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
     if (send) {
 #pragma unroll
       for (int j = 0; j < R; ++j)
-        if (j0 + j == tj) push_q(p, obc + j, q[j], 1u, srt, c[0]);
+        if (j0 + j == tj) {
+          push_q(p, obc + j, q[j], 1u, srt, c[0]);
+          gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[obc + j].x, 1);  // node.go:118
+        }
     }
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -641,7 +664,10 @@ __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, i
       }
       push_q(p, ob + j, q, kGMarker | sid, receive_time(p, broadcast_draw(p, s0) + (unsigned long long)j, t), c[0]);
     }
-    if (send && j == tj) push_q(p, ob + j, q, 1u, receive_time(p, send_draw(p, v), t), c[0]);
+    if (send && j == tj) {
+      push_q(p, ob + j, q, 1u, receive_time(p, send_draw(p, v), t), c[0]);
+      gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[ob + j].x, 1);  // node.go:118
+    }
     p.hq[ob + j] = q;
   }
 }
@@ -674,6 +700,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
       // SendTokens(v, out-link j, 1): node.go:112-131 (one channel: no batching)
       p.tokens[v] = tok - 1;
       push_entry(p, ob + tj, 1u, receive_time(p, send_draw(p, v), t), c[0]);
+      gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[ob + tj].x, 1);  // node.go:118
     }
   }
   const int idx[2] = {GC_PUSH, GC_PEEK};
@@ -749,7 +776,10 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
             if (p.route[obv + mid].x < op.b) lo = mid + 1;
             else hi = mid;
           }
-          if (op.b < 0 || lo >= od || p.route[obv + lo].x != op.b) {
+          const bool link = op.b >= 0 && lo < od && p.route[obv + lo].x == op.b;
+          // SentMsgRecord (node.go:118): after the balance check, before the link check
+          gtrace(p, time, kTrHost, (uint32_t)(ob + i), 0u, TK_SENT_TOKEN, v, link ? op.b : -1, op.n);
+          if (!link) {
             set_status(p.sc, ST_FATAL_UNKNOWN_DEST);
           } else {
             const unsigned long long d = p.sc->draw++;
@@ -766,6 +796,9 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
       for (int32_t k = lo + (int32_t)threadIdx.x; k < hi; k += blockDim.x)
         rec[k] = (uint64_t)p.chin[k].tokcnt | ((uint64_t)kOpen << 32);
       if (threadIdx.x == 0) {
+        gtrace(p, time, kTrHost, (uint32_t)(ob + i), 0u, TK_START, v, -1, sid);  // sim.go:109
+        for (int32_t j = 0; j < od && p.trace; ++j)  // SendToNeighbors (node.go:100)
+          gtrace(p, time, kTrHost, (uint32_t)(ob + i), 1u + (uint32_t)j, TK_SENT_MARKER, v, p.route[obv + j].x, sid);
         const size_t sv = (size_t)sid * p.n + v;
         p.W[sv] = ((uint64_t)(uint32_t)time << 32) | 0xffffffffull;
         p.stok[sv] = p.tokens[v];

@@ -54,6 +54,12 @@ constexpr int32_t kMaxDegree = 127;     // 7-bit out-index in a pick word
 constexpr int32_t kWave = 64;
 constexpr int32_t kWavesPerBlock = 4;
 constexpr int32_t kMaxLdsBytes = 160 * 1024;
+// Degree bounds up to this unroll the kernel's per-node loops with the in-link words in
+// registers (cl_kernels.hip unrolled()); larger ones keep them in the lane's LDS column.
+#ifndef CLSNAP_UNROLL_MAX
+#define CLSNAP_UNROLL_MAX 4
+#endif
+constexpr int32_t kUnrollMaxD = CLSNAP_UNROLL_MAX;
 
 // ---- device event trace (the reference's debug Logger, logger.go:12-76) -------
 // One 16-byte record per LogEvent.  Records of an instance are appended unordered and
@@ -138,7 +144,10 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
   L.w_chw = od << cap_log2;
   L.w_cur = L.w_chw + od;
   L.w_int = L.w_cur + id;
-  L.w_pend = L.w_int + id;
+  // in-link words live in registers when the kernel's degree bound is unrolled
+  const int32_t dmax = od > id ? od : id;
+  const int32_t dbound = dmax <= 1 ? 1 : dmax <= 2 ? 2 : dmax <= 4 ? 4 : 8;
+  L.w_pend = L.w_int + (dbound <= kUnrollMaxD ? 0 : id);
   L.w_trig = L.w_pend + L.sp;
   L.priv = L.w_trig + id;
   const int32_t base = L.priv * kWave;

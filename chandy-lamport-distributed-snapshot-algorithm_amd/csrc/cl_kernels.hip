@@ -126,9 +126,6 @@ struct Lane {
 //   CLSNAP_UNROLL_MAX  largest D whose loops are unrolled with in-link words in registers
 //   CLSNAP_A_PRED      phase A (pick) as predicated straight-line code (1) or branches (0)
 //   CLSNAP_B_PRED      phase B (receive) likewise
-#ifndef CLSNAP_UNROLL_MAX
-#define CLSNAP_UNROLL_MAX 4
-#endif
 #ifndef CLSNAP_A_PRED
 #define CLSNAP_A_PRED 1
 #endif

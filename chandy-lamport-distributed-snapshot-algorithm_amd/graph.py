@@ -12,7 +12,7 @@ import ctypes as C
 
 import numpy as np
 
-from . import (ClSnapError, GlobalSnapshot, MsgSnapshot, PassTokenEvent, SnapshotEvent, _check, _p,
+from . import (ClSnapError, GlobalSnapshot, MsgSnapshot, PassTokenEvent, SnapshotEvent, _check, _p, format_log,
                COUNTER_NAMES, lib)
 
 GSUM_NAMES = ("ok", "delivered", "completed", "cut_residual", "final_residual", "digest", "in_flight")
@@ -43,6 +43,8 @@ def glib():
             "cl_graph_node_id": [vp, i32, vp, i32],
             "cl_graph_node_id_length": [vp, i32, vp],
             "cl_graph_set_push_lanes": [vp, i32],
+            "cl_graph_trace_enable": [vp, i32],
+            "cl_graph_trace_read": [vp, vp, i32, vp],
             "cl_graph_set_limits": [vp, i32, i32, i64],
             "cl_graph_set_delay_hash": [vp, u64],
             "cl_graph_set_delay_go_seed": [vp, i64],
@@ -300,3 +302,21 @@ class GraphSim:
         out = np.zeros(len(GSUM_NAMES), dtype=np.int64)
         _check(self._L.cl_graph_get_checksums(self._h, _p(out)))
         return dict(zip(GSUM_NAMES, out.tolist()))
+
+    # ---- device event trace: the reference's debug Logger (logger.go:12-76) ------------
+    def trace_enable(self, capacity=1 << 16):
+        """Record the Logger from the next run on (capacity records; 0 = off)."""
+        _check(self._L.cl_graph_trace_enable(self._h, capacity))
+
+    def trace(self):
+        """LogEvents in Logger order: (epoch, kind, node rank, other rank | -1, data,
+        nodeTokens); kinds LOG_* (include/clsnap.h CL_LOG_*)."""
+        n = C.c_int32(0)
+        _check(self._L.cl_graph_trace_read(self._h, None, 0, C.byref(n)))
+        out = np.zeros((max(n.value, 1), 6), dtype=np.int32)
+        _check(self._L.cl_graph_trace_read(self._h, _p(out), n.value, C.byref(n)))
+        return [tuple(int(x) for x in r) for r in out[:n.value]]
+
+    def pretty_print(self):
+        """Logger.PrettyPrint (logger.go:55-64) as text."""
+        return format_log(self.node_ids(), self.trace())

@@ -143,6 +143,17 @@ int cl_graph_collect_snapshot(cl_graph* g, int32_t sid, int64_t* tokens, int64_t
 int cl_graph_get_counters(cl_graph* g, int64_t* out /* [CL_NUM_COUNTERS] */);
 int cl_graph_get_checksums(cl_graph* g, int64_t* out /* [CL_NUM_GSUMS] */);
 
+/* ---- device event trace: the reference's debug Logger (logger.go:12-76) ---------- */
+/* Record up to `capacity` LogEvents from the next run on (0 = off, the default); the next
+ * flush replays the program with tracing.  A debugging aid: records go through one device
+ * counter, so keep it to graphs and runs of modest size. */
+int cl_graph_trace_enable(cl_graph* g, int32_t capacity);
+/* The Logger's records (cl_log_event, clsnap.h) in its order -- per epoch (simulator time),
+ * the tick's deliveries in sender rank order with the broadcasts and EndSnapshot records
+ * they cause, then that step's traffic sends in node order, then the host events -- with
+ * LogEvent.nodeTokens.  *n_events = total; CL_E_LIMIT if the run overflowed the capacity. */
+int cl_graph_trace_read(cl_graph* g, cl_log_event* out, int32_t cap, int32_t* n_events);
+
 /* ---- counter hash of the synthetic workloads ------------------------------------ */
 uint64_t cl_counter_hash(uint64_t seed, uint64_t a, uint64_t b);
 
