@@ -522,7 +522,7 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
 #define CLSNAP_W2 0
 #endif
 #ifndef CLSNAP_W4
-#define CLSNAP_W4 0
+#define CLSNAP_W4 5  // D = 4 (8nodes-concurrent, BASELINE config 3): 5 waves/SIMD, DESIGN.md §9
 #endif
 constexpr int waves_for(int D) {
   return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1) : D == 4 ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : 1;
