@@ -109,6 +109,10 @@ struct GScal {
   int32_t dleft;    // extra ticks left in phase 1
   int32_t dticks;   // ticks spent waiting
   int32_t dcur;     // first snapshot (< the drain's count) not yet complete
+  // parallel send group (k_sg_check -> k_sg_apply)
+  int32_t sg_first;              // position of the group's first failing send (INT32_MAX: none)
+  int32_t pad2;
+  unsigned long long sg_draw0;   // the group's first draw index
 };
 enum : int32_t { kDrainWait = 0, kDrainExtra = 1, kDrainDone = 2, kDrainHang = 3 };
 constexpr int32_t kTimeFromDevice = -1;
@@ -181,6 +185,10 @@ int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain,
 int cg_launch_drain_end(const GParams& p, void* stream);  // normal ticks run again
 int cg_launch_sends(const GParams& p, int32_t t, void* stream);  // step-0 traffic
 int cg_launch_hostops(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream);
+// A run of host sends from pairwise distinct senders, in parallel: no send of the run
+// changes another's sender balance or channel, so every send up to the first failing one
+// (program order) executes at once with draw index d + position.
+int cg_launch_sendgroup(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream);
 // Recorded copies on channels still recording at the end (out[0] += ...).
 int cg_launch_finish(const GParams& p, int32_t n_sids, unsigned long long* out, void* stream);
 // Batch checks (out zeroed by the caller, 3 + n_sids entries): out[0] final node tokens,

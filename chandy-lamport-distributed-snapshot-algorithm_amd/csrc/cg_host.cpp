@@ -77,7 +77,9 @@ struct GBuf {
   size_t bytes() const { return n * sizeof(T); }
 };
 
-enum ProgKind : int32_t { P_SEND = 1, P_SNAP = 2, P_TICK = 3, P_DRAIN = 4 };
+// P_HOST: n consecutive host events (gops, in order); P_TICK: n ticks; P_DRAIN: a = snapshots
+// started before the drain.
+enum ProgKind : int32_t { P_HOST = 1, P_TICK = 3, P_DRAIN = 4 };
 struct ProgOp {
   int32_t kind, a, b;
   int64_t n;
@@ -206,6 +208,22 @@ struct cl_graph {
     return ids[by_rank[r]];
   }
 
+  // rank of an id given as a view (no allocation for ids of up to 15 bytes: std::string SSO)
+  int32_t rank_of_sv(std::string_view id) const {
+    if (bulk) {
+      if (id.size() != (size_t)id_width + 1 || id[0] != 'N') return -1;
+      int64_t v = 0;
+      for (size_t i = 1; i < id.size(); ++i) {
+        if (id[i] < '0' || id[i] > '9') return -1;
+        v = v * 10 + (id[i] - '0');
+      }
+      return v < n ? (int32_t)v : -1;
+    }
+    auto it = id_index.find(std::string(id));
+    if (it == id_index.end()) return -1;
+    return frozen ? rank_of[it->second] : it->second;
+  }
+
   // rank of an id, -1 if unknown
   int32_t rank_of_id(const char* id) const {
     if (!id) return -1;
@@ -323,16 +341,25 @@ struct cl_graph {
       if (it != hi && *it == b) ch_sends[it - ch_dst.begin()]++;
     }
     host_sends++;
-    prog.push_back(ProgOp{P_SEND, a, b, nt});
+    append_host();
     gops.push_back(GOp{GOP_SEND, a, b, (int32_t)nt});
     return CL_OK;
+  }
+
+  // one more host event in the program (runs of them share one program op)
+  void append_host() {
+    if (!prog.empty() && prog.back().kind == P_HOST && executed < prog.size()) {
+      prog.back().n += 1;
+      return;
+    }
+    prog.push_back(ProgOp{P_HOST, 0, 0, 1});
   }
 
   int append_snap(int32_t a, int32_t* out_sid) {
     if (n_sids == INT32_MAX) return gerr(CL_E_LIMIT, "too many snapshots");
     const int32_t sid = n_sids++;
     if (out_sid) *out_sid = sid;
-    prog.push_back(ProgOp{P_SNAP, a, sid, 0});
+    append_host();
     gops.push_back(GOp{GOP_SNAP, a, sid, 0});
     return CL_OK;
   }
@@ -504,10 +531,36 @@ struct cl_graph {
     return k_err(cg_launch_tick(P, (int32_t)time, stream));
   }
 
+  // Host events [pend_begin, +pend_count) in program order.  Maximal runs of at least
+  // kSendGroupMin sends from pairwise distinct senders (an event-file step of a large
+  // synthetic workload: one send line per node) run as one parallel send group; the rest
+  // runs through the sequential k_hostops.
+  static constexpr size_t kSendGroupMin = 64;
+  std::vector<uint32_t> seen_stamp;
+  uint32_t stamp = 0;
   int flush_hostops(size_t& pend_begin, size_t& pend_count) {
     if (!pend_count) return CL_OK;
-    int rc = k_err(cg_launch_hostops(P, (int32_t)time, (int32_t)pend_begin, (int32_t)pend_count, stream));
-    pend_begin += pend_count;
+    int rc = CL_OK;
+    const size_t end = pend_begin + pend_count;
+    if (seen_stamp.size() != (size_t)n) seen_stamp.assign((size_t)n, 0u);
+    size_t i = pend_begin, seq = pend_begin;  // [seq, i): sequential events not yet launched
+    while (i < end && rc == CL_OK) {
+      size_t j = i;
+      if (++stamp == 0) {
+        std::fill(seen_stamp.begin(), seen_stamp.end(), 0u);
+        stamp = 1;
+      }
+      while (j < end && gops[j].kind == GOP_SEND && seen_stamp[gops[j].a] != stamp) seen_stamp[gops[j].a] = stamp, ++j;
+      if (j - i >= kSendGroupMin) {
+        if (i > seq) rc = k_err(cg_launch_hostops(P, (int32_t)time, (int32_t)seq, (int32_t)(i - seq), stream));
+        if (rc == CL_OK) rc = k_err(cg_launch_sendgroup(P, (int32_t)time, (int32_t)i, (int32_t)(j - i), stream));
+        i = seq = j;
+      } else {
+        i = std::max(j, i + 1);
+      }
+    }
+    if (rc == CL_OK && end > seq) rc = k_err(cg_launch_hostops(P, (int32_t)time, (int32_t)seq, (int32_t)(end - seq), stream));
+    pend_begin = end;
     pend_count = 0;
     return rc;
   }
@@ -585,8 +638,8 @@ struct cl_graph {
     // never execute (the oracle and the multi-instance engine stop there too)
     for (size_t i = begin; i < prog.size() && !hang; ++i) {
       const ProgOp& op = prog[i];
-      if (op.kind == P_SEND || op.kind == P_SNAP) {
-        ++pend_count;
+      if (op.kind == P_HOST) {
+        pend_count += (size_t)op.n;
       } else if (op.kind == P_TICK) {
         if ((rc = flush_hostops(pend_begin, pend_count))) return rc;
         for (int64_t k = 0; k < op.n; ++k)
@@ -709,27 +762,92 @@ int cl_graph_add_link(cl_graph* g, const char* src, const char* dest) {
   return CL_OK;
 }
 
+// readTopologyFile (test_common.go:29-68), streaming over the text without per-line copies:
+// lines starting with '#' are comments (:41), the first other line is the node count, the
+// next `count` lines "id tokens" are AddNode calls, every later line "src dest" an AddLink.
+// The link section -- 8.4M lines for BASELINE config 4 -- is parsed by all host threads
+// over newline-aligned chunks (read-only id lookups) and appended in file order; the
+// first error in file order is the one reported, as in a sequential parse.
 int cl_graph_read_topology_text(cl_graph* g, const char* text) {
   G_CHECK(g);
   if (!text) return gerr(CL_E_INVALID, "null text");
+  const std::string_view all(text);
+  LineIter it{all};
+  std::string_view line, f[3];
   int64_t left = -1;
-  for (const std::string& line : go_lines(text)) {
-    if (!line.empty() && line[0] == '#') continue;
+  size_t link_start = all.size();
+  while (it.next(&line)) {
+    if (line[0] == '#') continue;
     if (left < 0) {
-      if (!go_atoi(line, &left)) return gerr(CL_E_PARSE, "bad node count line: %s", line.c_str());
+      if (!go_atoi_sv(line, &left)) return gerr(CL_E_PARSE, "bad node count line: %.*s", (int)line.size(), line.data());
+      if (left == 0) {
+        link_start = it.i;
+        break;
+      }
       continue;
     }
-    auto f = go_fields(line);
-    if (f.size() != 2) return gerr(CL_E_PARSE, "Expected 2 tokens in line: %s", line.c_str());
-    int rc;
-    if (left > 0) {
-      int64_t tok;
-      if (!go_atoi(f[1], &tok)) return gerr(CL_E_PARSE, "bad token count: %s", f[1].c_str());
-      if ((rc = cl_graph_add_node(g, f[0].c_str(), tok))) return rc;
-      left--;
-    } else if ((rc = cl_graph_add_link(g, f[0].c_str(), f[1].c_str()))) {
-      return rc;
+    if (go_fields_sv(line, f, 3) != 2)
+      return gerr(CL_E_PARSE, "Expected 2 tokens in line: %.*s", (int)line.size(), line.data());
+    int64_t tok;
+    if (!go_atoi_sv(f[1], &tok)) return gerr(CL_E_PARSE, "bad token count: %.*s", (int)f[1].size(), f[1].data());
+    int rc = cl_graph_add_node(g, std::string(f[0]).c_str(), tok);
+    if (rc) return rc;
+    if (--left == 0) {
+      link_start = it.i;
+      break;
     }
+  }
+  if (link_start >= all.size()) return CL_OK;
+  if (g->frozen) return gerr(CL_E_STATE, "topology changes after events are not supported");
+  // ---- the link section, in parallel ----
+  const std::string_view rest = all.substr(link_start);
+  const int T = (int)std::max<size_t>(1, std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()),
+                                                           rest.size() / (1 << 20) + 1));
+  std::vector<size_t> cut(T + 1, rest.size());
+  cut[0] = 0;
+  for (int t = 1; t < T; ++t) {  // chunk boundaries just after a newline
+    size_t c = rest.size() * t / T;
+    const size_t nl = rest.find('\n', c);
+    cut[t] = nl == std::string_view::npos ? rest.size() : nl + 1;
+    if (cut[t] < cut[t - 1]) cut[t] = cut[t - 1];
+  }
+  struct Part {
+    std::vector<std::pair<int, int>> links;
+    size_t err_pos = SIZE_MAX;
+    int err_code = 0;
+    std::string err;
+  };
+  std::vector<Part> parts(T);
+  auto lookup = [&](std::string_view id) -> int {
+    auto f2 = g->id_index.find(std::string(id));
+    return f2 == g->id_index.end() ? -1 : f2->second;
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      Part& P = parts[t];
+      LineIter li{rest.substr(0, cut[t + 1]), cut[t]};
+      std::string_view ln, ff[3];
+      while (li.next(&ln)) {
+        if (ln[0] == '#') continue;
+        const size_t pos = (size_t)(ln.data() - rest.data());
+        if (go_fields_sv(ln, ff, 3) != 2) {
+          P.err_pos = pos, P.err_code = CL_E_PARSE, P.err = "Expected 2 tokens in line: " + std::string(ln);
+          return;
+        }
+        const int a = lookup(ff[0]), b = a < 0 ? -1 : lookup(ff[1]);
+        if (a < 0 || b < 0) {  // sim.go:49-54 log.Fatalf("Node %v does not exist")
+          P.err_pos = pos, P.err_code = CL_E_UNKNOWN_NODE;
+          P.err = "Node " + std::string(a < 0 ? ff[0] : ff[1]) + " does not exist";
+          return;
+        }
+        if (a != b) P.links.emplace_back(a, b);  // node.go:88-90
+      }
+    });
+  for (auto& x : th) x.join();
+  for (int t = 0; t < T; ++t) {  // file order: links of earlier chunks, then the first error
+    g->links.insert(g->links.end(), parts[t].links.begin(), parts[t].links.end());
+    if (parts[t].err_code) return gerr(parts[t].err_code, "%s", parts[t].err.c_str());
   }
   return CL_OK;
 }
@@ -969,30 +1087,41 @@ int cl_graph_drain(cl_graph* g) {
   return CL_OK;
 }
 
+// readEventsFile (test_common.go:79-140) incl. the drain, streaming over the text: the
+// event lines of a large synthetic workload (one `send` line per sending node and step)
+// append to the program without per-line copies; runs of sends from distinct senders
+// execute as parallel send groups (cg_launch_sendgroup).
 int cl_graph_read_events_text(cl_graph* g, const char* text, int32_t* n_snapshots) {
   G_CHECK(g);
   if (!text) return gerr(CL_E_INVALID, "null text");
+  int rc = g->freeze();
+  if (rc) return rc;
   int32_t snaps = 0;
-  for (const std::string& line : go_lines(text)) {
+  LineIter it{std::string_view(text)};
+  std::string_view line, f[4];
+  while (it.next(&line)) {
     if (line == "#") continue;  // strings.HasPrefix("#", line) (test_common.go:90, sic)
-    auto f = go_fields(line);
-    if (f.empty()) return gerr(CL_E_PARSE, "empty event line");
-    int rc;
+    const int nf = go_fields_sv(line, f, 4);
+    if (nf == 0) return gerr(CL_E_PARSE, "empty event line");
     if (f[0] == "send") {
       int64_t nt;
-      if (f.size() < 4 || !go_atoi(f[3], &nt)) return gerr(CL_E_PARSE, "bad send line: %s", line.c_str());
-      rc = cl_graph_send_tokens(g, f[1].c_str(), f[2].c_str(), nt);
+      if (nf < 4 || !go_atoi_sv(f[3], &nt)) return gerr(CL_E_PARSE, "bad send line: %.*s", (int)line.size(), line.data());
+      const int32_t a = g->rank_of_sv(f[1]);
+      if (a < 0) return gerr(CL_E_UNKNOWN_NODE, "send from unknown node %.*s", (int)f[1].size(), f[1].data());
+      rc = g->append_send(a, g->rank_of_sv(f[2]), nt);  // unknown dest: fatal at run time (node.go:121-124)
     } else if (f[0] == "snapshot") {
-      if (f.size() < 2) return gerr(CL_E_PARSE, "bad snapshot line: %s", line.c_str());
+      if (nf < 2) return gerr(CL_E_PARSE, "bad snapshot line: %.*s", (int)line.size(), line.data());
       snaps++;
-      rc = cl_graph_start_snapshot(g, f[1].c_str(), nullptr);
+      const int32_t a = g->rank_of_sv(f[1]);
+      if (a < 0) return gerr(CL_E_UNKNOWN_NODE, "snapshot at unknown node %.*s", (int)f[1].size(), f[1].data());
+      rc = g->append_snap(a, nullptr);
     } else if (f[0] == "tick") {
       int64_t nt = 1;
-      if (f.size() > 1 && !go_atoi(f[1], &nt)) return gerr(CL_E_PARSE, "bad tick line: %s", line.c_str());
+      if (nf > 1 && !go_atoi_sv(f[1], &nt)) return gerr(CL_E_PARSE, "bad tick line: %.*s", (int)line.size(), line.data());
       if (nt > INT32_MAX) return gerr(CL_E_LIMIT, "tick count too large");
-      rc = cl_graph_tick(g, (int32_t)std::max<int64_t>(nt, 0));
+      rc = g->append_tick(std::max<int64_t>(nt, 0));
     } else {
-      return gerr(CL_E_PARSE, "Unknown event command: %s", f[0].c_str());
+      return gerr(CL_E_PARSE, "Unknown event command: %.*s", (int)f[0].size(), f[0].data());
     }
     if (rc) return rc;
   }

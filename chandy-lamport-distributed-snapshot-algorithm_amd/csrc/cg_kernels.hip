@@ -818,6 +818,61 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
 }
 
 // ---------------------------------------------------------------------------
+// a run of host sends from pairwise distinct senders (cg_launch_sendgroup)
+// ---------------------------------------------------------------------------
+// SendTokens' failure of send i (node.go:112-131): 1 insufficient tokens, 2 unknown dest;
+// *c = the channel of a send that passes.
+__device__ inline int send_check(const GParams& p, const GOp& op, int32_t* c) {
+  const int32_t v = op.a;
+  if (p.tokens[v] < op.n) return 1;
+  const int32_t obv = p.out_off[v], od = p.out_off[v + 1] - obv;
+  int32_t lo = 0, hi = od;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (p.route[obv + mid].x < op.b) lo = mid + 1;
+    else hi = mid;
+  }
+  if (op.b < 0 || lo >= od || p.route[obv + lo].x != op.b) return 2;
+  *c = obv + lo;
+  return 0;
+}
+
+__global__ void __launch_bounds__(kGThreads) k_sg_check(GParams p, int32_t ob, int32_t oc) {
+  const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
+  if (i == 0) p.sc->sg_draw0 = p.sc->draw;
+  if (i >= oc || p.sc->status) return;
+  int32_t c;
+  if (send_check(p, p.ops[ob + i], &c)) atomicMin(&p.sc->sg_first, i);
+}
+
+__global__ void __launch_bounds__(kGThreads) k_sg_apply(GParams p, int32_t time, int32_t ob, int32_t oc) {
+  const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
+  unsigned long long pushes = 0;
+  if (p.sc->status == 0 && i < oc) {
+    const int32_t first = p.sc->sg_first;
+    const unsigned long long d0 = p.sc->sg_draw0;
+    if (i == 0) p.sc->draw = d0 + (unsigned long long)(first < oc ? first : oc);  // draws of the sends that ran
+    const GOp op = p.ops[ob + i];
+    int32_t c = -1;
+    const int fail = i <= first ? send_check(p, op, &c) : 0;
+    if (i < first) {  // SentMsgRecord (node.go:118), tokens -= n, Queue.Push with draw d0 + i
+      gtrace(p, time, kTrHost, (uint32_t)(ob + i), 0u, TK_SENT_TOKEN, op.a, op.b, op.n);
+      p.tokens[op.a] -= op.n;
+      push_entry(p, c, (uint32_t)op.n, receive_time(p, d0 + (unsigned long long)i, time), pushes);
+    } else if (i == first) {  // the first failure freezes the run exactly where the program does
+      if (fail == 1) {
+        set_status(p.sc, ST_FATAL_INSUFFICIENT);
+      } else {  // logged and debited before the link check (node.go:118-124)
+        gtrace(p, time, kTrHost, (uint32_t)(ob + i), 0u, TK_SENT_TOKEN, op.a, -1, op.n);
+        p.tokens[op.a] -= op.n;
+        set_status(p.sc, ST_FATAL_UNKNOWN_DEST);
+      }
+    }
+  }
+  wave_count(&p.cpart[GC_PUSH], pushes);
+}
+
+// ---------------------------------------------------------------------------
 // results
 // ---------------------------------------------------------------------------
 // Recorded copies of channels still recording at the end (HandleToken appended them).
@@ -961,6 +1016,17 @@ int cg_launch_drain_end(const GParams& p, void* stream) {
 
 int cg_launch_hostops(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream) {
   hipLaunchKernelGGL(k_hostops, dim3(1), dim3(kThreads), 0, (hipStream_t)stream, p, time, op_begin, op_count);
+  return hipGetLastError();
+}
+
+__global__ void k_sg_begin(GParams p) { p.sc->sg_first = 0x7fffffff; }
+
+int cg_launch_sendgroup(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = (unsigned)((op_count + kGThreads - 1) / kGThreads);
+  hipLaunchKernelGGL(k_sg_begin, dim3(1), dim3(1), 0, s, p);
+  hipLaunchKernelGGL(k_sg_check, dim3(g), dim3(kGThreads), 0, s, p, op_begin, op_count);
+  hipLaunchKernelGGL(k_sg_apply, dim3(g), dim3(kGThreads), 0, s, p, time, op_begin, op_count);
   return hipGetLastError();
 }
 

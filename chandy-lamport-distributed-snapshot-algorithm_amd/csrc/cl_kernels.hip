@@ -67,7 +67,6 @@ struct Ctx {
   int32_t indeg, outdeg, out_off;
   // snapshot outputs by 32-bit byte offsets from the (uniform) array bases: the stores use
   // the SGPR-base + 32-bit-VGPR-offset form, with no 64-bit address arithmetic per store
-  uint32_t tok_lane, rec_lane, tick_lane;  // this lane's byte offset in sid plane 0
   uint32_t tok_plane, rec_plane, tick_plane;  // bytes per sid plane (uniform)
   bool mul24;  // every plane offset sid * plane fits the 24-bit multiplier
 };
@@ -77,6 +76,10 @@ struct Ctx {
 __device__ __forceinline__ uint32_t plane_off(const Ctx& x, uint32_t sid, uint32_t plane) {
   return x.mul24 ? __umul24(sid, plane) : sid * plane;
 }
+// This lane's byte offsets in snapshot plane 0, recomputed at each store (cheaper than
+// keeping them live in VGPRs through the tick loop).
+__device__ __forceinline__ uint32_t tok_lane(const Ctx& x) { return 4u * (x.inst * (uint32_t)x.p.n_nodes + (uint32_t)x.v); }
+__device__ __forceinline__ uint32_t rec_lane(const Ctx& x) { return 4u * x.inst * (uint32_t)x.p.n_ch; }
 template <class T>
 __device__ __forceinline__ void st_at(T* base, uint32_t byte_off, T val) {
   *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off) = val;
@@ -106,7 +109,8 @@ struct Lane {
   int32_t tokens;
   uint32_t started;
   int32_t time, draw, status;
-  uint32_t peek, pop_tok, pop_mk, push;
+  uint32_t peek, push;
+  uint32_t pops;  // packets this node delivered as a sender: tokens (lo16) | markers (hi16); <= 1 per tick
   bool alive;    // instance still running (uniform within the segment)
   int32_t flag;  // lane-local engine failure raised during an op/tick
 #if CLSNAP_PROF
@@ -203,8 +207,8 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
                                              int32_t arrive) {
   const ExecParams& p = x.p;
   const Layout& lay = x.lay;
-  st_at(p.snap_tok, plane_off(x, (uint32_t)sid, x.tok_plane) + x.tok_lane, ln.tokens);
-  const uint32_t rb = plane_off(x, (uint32_t)sid, x.rec_plane) + x.rec_lane;
+  st_at(p.snap_tok, plane_off(x, (uint32_t)sid, x.tok_plane) + tok_lane(x), ln.tokens);
+  const uint32_t rb = plane_off(x, (uint32_t)sid, x.rec_plane) + rec_lane(x);
   if constexpr (unrolled(D)) {
 #pragma unroll
     for (int32_t kj = 0; kj < D; ++kj) {
@@ -226,7 +230,7 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
 __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
   const uint32_t old = lds_add(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
   if (old + 1 == (uint32_t)x.p.n_nodes) {
-    st_at(x.p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + x.tick_lane, ln.time);
+    st_at(x.p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + 4u * x.inst, ln.time);
     lds_add(&XW(x.lay.x_ndone + x.seg), 1u);
   }
 }
@@ -277,7 +281,7 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
   } else {  // later marker: stop recording this channel
     // hi16 of the cursor word: the channel's end
     st_at(reinterpret_cast<uint16_t*>(x.p.snap_rec),
-          plane_off(x, (uint32_t)sid, x.rec_plane) + x.rec_lane + ((w >> 16) << 2) + 2u,
+          plane_off(x, (uint32_t)sid, x.rec_plane) + rec_lane(x) + ((w >> 16) << 2) + 2u,
           (uint16_t)PW(lay.w_cur + ki));
     pend = ((pw >> sh) & 0xffu) - 1;
   }
@@ -356,6 +360,8 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
     }
   }
   XW(lay.x_pick + x.lane) = pick;
+  // Queue.Pop (sim.go:85), counted at the sender: at most one per tick, so 16 bits each
+  ln.pops += (pick & kPickValid) ? ((pick & kMarkerBit) ? 0x10000u : 1u) : 0u;
   wave_sync();
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
@@ -374,8 +380,6 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
         if (m) temit<TRACE>(x, mk ? TK_RECV_MARKER : TK_RECV_TOKEN, src, ln.time, src << 8, (int32_t)pay, ln.tokens);
       // HandleToken: tokens += data; the channel's recording cursor advances
       ln.tokens += tok ? (int32_t)pay : 0;
-      ln.pop_tok += tok ? 1u : 0u;
-      ln.pop_mk += mk ? 1u : 0u;
       const uint32_t cur = PW(lay.w_cur + ki);
       PW(lay.w_cur + ki) = cur + (tok ? 1u : 0u);
       if (mk) handle_marker<D, TRACE>(x, ln, it, ki, w, src, (int32_t)pay, ntrig);
@@ -392,12 +396,10 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       temit<TRACE>(x, (pk & kMarkerBit) ? TK_RECV_MARKER : TK_RECV_TOKEN, src, ln.time, src << 8, (int32_t)pay,
                    ln.tokens);
       if (!(pk & kMarkerBit)) {  // HandleToken: tokens += data; the recording cursor advances
-        ln.pop_tok++;
         ln.tokens += (int32_t)pay;
         PW(lay.w_cur + ki) += 1u;
         continue;
       }
-      ln.pop_mk++;
       handle_marker<D, TRACE>(x, ln, it, ki, w, src, (int32_t)pay, ntrig);
     }
   }
@@ -525,7 +527,8 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
 #define CLSNAP_W4 5  // D = 4 (8nodes-concurrent, BASELINE config 3): 5 waves/SIMD, DESIGN.md §9
 #endif
 constexpr int waves_for(int D) {
-  return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1) : D == 4 ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : 1;
+  return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1)
+         : (D == 3 || D == 4) ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : 1;
 }
 
 template <int D, bool STAGED, bool TRACE>
@@ -560,7 +563,6 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   const uint32_t C = (uint32_t)p.n_ch;
   const Ctx x{p, lay, X + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0,
-              4u * (ii * (uint32_t)N + (uint32_t)v), 4u * ii * C, 4u * ii,
               4u * st * (uint32_t)N, 4u * st * C, 4u * st,
               4ull * st * (uint64_t)max(N, (int32_t)C) < (1ull << 24)};
   InLinks<D> it;
@@ -583,7 +585,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     // orders these stores before any completion store of the same wave
     if (valid)
       for (int32_t sid = v; sid < lay.s_cap; sid += N)
-        st_at(p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + x.tick_lane, (int32_t)-1);
+        st_at(p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + 4u * x.inst, (int32_t)-1);
     // HBM spill ring heads start at 0 likewise: every lane owns its out-channels' heads
     // (only their sender pushes, refills and counts them)
     if (valid && lay.ocap_log2 >= 0)
@@ -593,7 +595,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     ln.tokens = valid ? (int32_t)topo[(size_t)N * p.topo_w + v] : 0;
     ln.started = 0;
     ln.time = ln.draw = ln.status = 0;
-    ln.peek = ln.pop_tok = ln.pop_mk = ln.push = 0;
+    ln.peek = ln.pops = ln.push = 0;
   } else {
     const uint32_t* S = p.state + ii;
     const uint32_t b = (uint32_t)v * (lay.priv + G_NUM);
@@ -605,8 +607,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     ln.draw = valid ? (int32_t)R[G_DRAW * st] : 0;
     ln.status = valid ? (int32_t)R[G_STATUS * st] : 0;
     ln.peek = valid ? R[G_PEEK * st] : 0;
-    ln.pop_tok = valid ? R[G_POP_TOK * st] : 0;
-    ln.pop_mk = valid ? R[G_POP_MK * st] : 0;
+    ln.pops = valid ? (R[G_POP_TOK * st] | (R[G_POP_MK * st] << 16)) : 0;
     ln.push = valid ? R[G_PUSH * st] : 0;
     wave_sync();
     if (valid && v == 0) {
@@ -707,8 +708,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   if (valid) {
     lds_u32* acc = &XW(lay.x_acc + 5 * seg);
     lds_add(acc + 0, ln.peek);
-    lds_add(acc + 1, ln.pop_tok);
-    lds_add(acc + 2, ln.pop_mk);
+    lds_add(acc + 1, ln.pops & 0xffffu);
+    lds_add(acc + 2, ln.pops >> 16);
     lds_add(acc + 3, ln.push);
     lds_add(acc + 4, (uint32_t)inflight);
   }
@@ -746,8 +747,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   R[G_DRAW * st] = (uint32_t)ln.draw;
   R[G_STATUS * st] = (uint32_t)ln.status;
   R[G_PEEK * st] = ln.peek;
-  R[G_POP_TOK * st] = ln.pop_tok;
-  R[G_POP_MK * st] = ln.pop_mk;
+  R[G_POP_TOK * st] = ln.pops & 0xffffu;
+  R[G_POP_MK * st] = ln.pops >> 16;
   R[G_PUSH * st] = ln.push;
   if (v == 0) {
     uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
@@ -837,11 +838,12 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
                            : launch_exec_ds<D, false, false>(p, topo, ops, sched, stream);
 }
 
-// The kernel is instantiated for degree bounds 1, 2, 4, ... CLSNAP_MAX_D.
+// The kernel is instantiated for degree bounds 1, 2, 3, 4, 8, ... CLSNAP_MAX_D.
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
   const int32_t d = p.lay.od > p.lay.id ? p.lay.od : p.lay.id;  // D must bound every in- and out-degree
   if (d <= 1) return launch_exec_d<1>(p, topo, ops, sched, stream);
   if (d <= 2) return launch_exec_d<2>(p, topo, ops, sched, stream);
+  if (d <= 3) return launch_exec_d<3>(p, topo, ops, sched, stream);  // 8nodes (BASELINE config 3)
   if (d <= 4) return launch_exec_d<4>(p, topo, ops, sched, stream);
 #if CLSNAP_MAX_D >= 8
   if (d <= 8) return launch_exec_d<8>(p, topo, ops, sched, stream);
