@@ -63,9 +63,11 @@ def _snaps(n, snaps, seed):
     return ss, sr
 
 
-def oracle_program(p, drain=False, max_drain=10000):
+def oracle_program(p, drain=False, max_drain=10000, log=False):
     s = O.OracleSim()
     s.use_counter_hash(p.delay_seed)
+    if log:
+        s.log_enable()
     assert s.build_graph(p.tokens, p.src, p.dst, p.width()) == 0
     rc = s.run_program(p.steps, p.traffic_seed, p.thresh, p.traffic_steps, p.snap_step, p.snap_rank)
     if drain and rc == 0:
@@ -200,3 +202,28 @@ def scenario_oracle(top, events, seed):
     assert o.read_topology(os.path.join(TEST_DATA, top)) == 0
     o.read_events(os.path.join(TEST_DATA, events))
     return o
+
+
+def program_files(p, log):
+    """(.top text, .events text) that replay program p through readTopologyFile /
+    readEventsFile: per step the traffic sends the run made (the SENT_TOKEN records of
+    `log`, an oracle or engine Logger of the synthetic run, in order), the step's
+    snapshots, one tick.  readEventsFile's drain follows the last line."""
+    n = p.n
+    w = p.width()
+    name = lambda r: f"N{r:0{w}d}"  # noqa: E731
+    top = [f"{n}"] + [f"{name(r)} {int(p.tokens[r])}" for r in range(n)] + \
+        [f"{name(int(a))} {name(int(b))}" for a, b in zip(p.src, p.dst)]
+    sends = {}
+    for ep, kind, node, other, data, _ in log:
+        if kind == 0:    # LOG_SENT_TOKEN
+            sends.setdefault(ep, []).append(f"send {name(node)} {name(other)} {data}")
+    ev = []
+    si = 0
+    for k in range(p.steps):
+        ev.extend(sends.get(k, []))
+        while si < len(p.snap_step) and p.snap_step[si] == k:
+            ev.append(f"snapshot {name(int(p.snap_rank[si]))}")
+            si += 1
+        ev.append("tick")
+    return "\n".join(top) + "\n", "\n".join(ev) + "\n"

@@ -17,7 +17,7 @@ import pytest
 import graphgen as G
 import oracle as O
 from graphcheck import (clg, cl, compare, digest_from_oracle, engine_program, engine_summary, oracle_program,
-                        powerlaw_program, regular_program, scenario_engine, scenario_oracle, Program)
+                        powerlaw_program, program_files, regular_program, scenario_engine, scenario_oracle, Program)
 from snapcheck import assert_equal, check_tokens, read_snapshot_file, scenarios
 
 pytestmark = pytest.mark.gpu
@@ -377,3 +377,46 @@ def test_c5_full_size_properties():
     g.rerun()
     g.synchronize()
     assert g.checksums() == sums
+
+
+def test_event_file_driven_c4_shape_vs_oracle():
+    """a C4-shaped workload given as .top / .events files -- one
+    `send` line per traffic send (~1,000 per step, run as parallel send groups), the
+    snapshots, `tick` lines, then readEventsFile's drain -- read by the engine's
+    streaming parsers and by the oracle's readEventsFile restatement: bit-exact."""
+    p = regular_program(4096, steps=70, seed=12, snaps=((5, None), (9, 0), (20, None)))
+    o = oracle_program(p, log=True)
+    top, events = program_files(p, o.log())
+    assert events.count("send") > 50_000
+    ref = O.OracleSim()
+    ref.use_counter_hash(p.delay_seed)
+    assert ref.read_topology_text(top) == 0
+    assert ref.read_events_text(events) == 0
+    g = clg.GraphSim(fifo_slots=p.fifo_slots)
+    g.read_topology_text(top)
+    g.set_delay_hash(p.delay_seed)
+    assert g.read_events_text(events) == 3
+    g.flush()
+    compare(g, ref)
+    assert all(ref.complete(s) for s in range(3))
+    assert g.checksums()["digest"] == digest_from_oracle(ref)
+
+
+def test_event_file_driven_large_equals_synthetic_run():
+    """2^18 nodes, 24 steps: the same traffic as send lines (~1.5M, the Logger of the
+    synthetic run) replayed from files equals the synthetic device-driven run with its
+    drain -- checksums, counters, status, time."""
+    p = regular_program(1 << 18, steps=24, seed=14, snaps=((3, None), (4, 0)))
+    s = engine_program(p, run=False, drain=True)
+    s.trace_enable(1 << 24)
+    s.flush()
+    top, events = program_files(p, s.trace())
+    assert events.count("send") > 1_000_000
+    g = clg.GraphSim(fifo_slots=p.fifo_slots)
+    g.read_topology_text(top)
+    g.set_delay_hash(p.delay_seed)
+    g.read_events_text(events)
+    g.flush()
+    assert g.status() == s.status() == 0 and g.time() == s.time()
+    assert g.checksums() == s.checksums()
+    assert g.counters() == s.counters()

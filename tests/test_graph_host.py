@@ -167,3 +167,56 @@ def test_oracle_program_conserves_tokens(kind):
     assert done >= 1
     assert o.counters()["draws"] == o.counters()["push"]
     assert isinstance(digest_from_oracle(o), int)
+
+
+def _topology_text(n, src, dst, tokens=100, comments=False):
+    w = len(str(n - 1))
+    lines = [f"{n}"] + [f"N{r:0{w}d} {tokens}" for r in range(n)]
+    for i, (a, b) in enumerate(zip(src, dst)):
+        if comments and i % 100000 == 7:
+            lines.append("# a comment inside the link section")
+        lines.append(f"N{a:0{w}d} N{b:0{w}d}")
+    return "\n".join(lines) + "\n"
+
+
+def test_streaming_topology_parse_matches_bulk_topology():
+    """readTopologyFile over a C4-shaped text (2^17 nodes, ~1M link lines, comments,
+    self links and duplicate links): the streaming parser (parallel link section) builds
+    the same channels and ids as the bulk rank API."""
+    n = 1 << 17
+    ws, wd = G.regular_graph(n, 8, 99)
+    src = np.concatenate([ws, [5, 6, int(ws[0])]]).astype(np.int64)
+    dst = np.concatenate([wd, [5, 6, int(wd[0])]]).astype(np.int64)   # self links + a duplicate
+    g = clg.GraphSim()
+    g.read_topology_text(_topology_text(n, src, dst, comments=True))
+    b = clg.GraphSim()
+    b.set_topology(np.full(n, 100), src.astype(np.int32), dst.astype(np.int32), id_width=len(str(n - 1)))
+    gs, gd = _edges(g)
+    bs, bd = _edges(b)
+    np.testing.assert_array_equal(gs, bs)
+    np.testing.assert_array_equal(gd, bd)
+    assert g.node_ids()[:3] == b.node_ids()[:3] and g.node_ids()[-1] == b.node_ids()[-1]
+
+
+def test_streaming_topology_parse_reports_first_error_in_file_order():
+    """Errors in different parallel chunks: the one earlier in the file is reported,
+    with the reference's message (sim.go:49-54, test_common.go:51-53)."""
+    n = 1 << 16
+    ws, wd = G.regular_graph(n, 8, 3)
+    text = _topology_text(n, ws, wd)
+    lines = text.split("\n")
+    k1, k2 = int(len(lines) * 0.4), int(len(lines) * 0.8)
+    a = list(lines)
+    a[k1] = "N00001 Nxyz"          # unknown node, earlier
+    a[k2] = "N00001 N00002 N00003"  # three fields, later
+    g = clg.GraphSim()
+    with pytest.raises(cl.ClSnapError) as e:
+        g.read_topology_text("\n".join(a))
+    assert e.value.code == -2 and "Nxyz does not exist" in str(e.value)
+    b = list(lines)
+    b[k1] = "N00001 N00002 N00003"
+    b[k2] = "N00001 Nxyz"
+    g = clg.GraphSim()
+    with pytest.raises(cl.ClSnapError) as e:
+        g.read_topology_text("\n".join(b))
+    assert e.value.code == -4 and "Expected 2 tokens" in str(e.value)
