@@ -62,6 +62,13 @@ struct MDel {
   int32_t s0, v, k, sid;  // sender, receiver, in-position of the channel, snapshot id
 };
 
+// A delivery that crosses devices in the partitioned mode: sender, receiver, in-position,
+// payload word (kGMarker | sid, or token count).
+struct PDel {
+  int32_t s, v, k;
+  uint32_t pay;
+};
+
 // Per in-channel record, by in-CSR position (16 B, one access per delivery / per
 // expanded in-link).
 struct ChIn {
@@ -113,6 +120,8 @@ struct GScal {
   int32_t sg_first;              // position of the group's first failing send (INT32_MAX: none)
   int32_t pad2;
   unsigned long long sg_draw0;   // the group's first draw index
+  // partitioned mode: this device's tick totals (k_scan), global bases set by the host
+  unsigned long long tot_trig, tot_send;
 };
 enum : int32_t { kDrainWait = 0, kDrainExtra = 1, kDrainDone = 2, kDrainHang = 3 };
 constexpr int32_t kTimeFromDevice = -1;
@@ -170,7 +179,18 @@ struct GParams {
   GTraceRec* trace;
   uint32_t* trace_cnt;
   int32_t trace_cap;
+  // Graph-partitioned mode: this device owns node ranks [part_lo, part_hi)
+  // = pick blocks [blk_lo, blk_hi) (part_lo a multiple of kGThreads); whole-graph runs own
+  // everything (part 0, [0, n)).  Arrays stay graph-sized; a device touches its own rows.
+  int32_t part;
+  int32_t part_lo, part_hi, blk_lo, blk_hi;
   int32_t pad1;
+  PDel* outbox;          // [n] deliveries by owned senders to other devices' receivers
+  uint32_t* out_n;       // [4] 0 outbox rows, 1 remote markers, 2 reports
+  MDel* rmlist;          // [n] markers delivered to owned receivers by other devices' senders
+  int2* reports;         // [n] (s0, outdeg) broadcasts triggered by other devices' senders
+  int32_t* trigv;        // [n] broadcasts triggered by owned senders this tick (draws)
+  unsigned long long* rdraw;  // [n] first draw of broadcasts triggered by other devices' senders
 };
 
 // Launchers (cg_kernels.hip); return hipError_t as int.
@@ -189,6 +209,14 @@ int cg_launch_hostops(const GParams& p, int32_t time, int32_t op_begin, int32_t 
 // changes another's sender balance or channel, so every send up to the first failing one
 // (program order) executes at once with draw index d + position.
 int cg_launch_sendgroup(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream);
+// Partitioned mode, one tick = pick -> [exchange deliveries] -> receive -> [exchange
+// reports] -> tally -> [allgather totals] -> bases -> [exchange replies] -> push.
+int cg_launch_part_pick(const GParams& p, int32_t t, void* stream);
+int cg_launch_part_receive(const GParams& p, int32_t t, const PDel* in, int32_t n_in, void* stream);
+int cg_launch_part_tally(const GParams& p, int32_t step, const int2* rep, int32_t n_rep, void* stream);
+int cg_launch_part_bases(const GParams& p, int64_t trig_before, int64_t trig_all, int64_t send_before,
+                         int64_t send_all, const int32_t* s0, int32_t n, unsigned long long* draw0, void* stream);
+int cg_launch_part_push(const GParams& p, int32_t t, int32_t step, const long long* replies, int32_t n, void* stream);
 // Recorded copies on channels still recording at the end (out[0] += ...).
 int cg_launch_finish(const GParams& p, int32_t n_sids, unsigned long long* out, void* stream);
 // Batch checks (out zeroed by the caller, 3 + n_sids entries): out[0] final node tokens,

@@ -178,6 +178,17 @@ struct cl_graph {
   int32_t trace_cap = 0;
   GBuf<GTraceRec> d_trace;
   GBuf<uint32_t> d_trace_cnt;
+  // graph-partitioned mode (cl_graph_part_begin)
+  bool part = false;
+  int32_t part_lo = 0, part_hi = 0;
+  GBuf<PDel> d_outbox, d_inbox;
+  GBuf<uint32_t> d_out_n;
+  GBuf<MDel> d_rmlist;
+  GBuf<int2> d_reports, d_rep_in;
+  GBuf<int32_t> d_trigv, d_s0;
+  GBuf<unsigned long long> d_rdraw, d_draw0;
+  GBuf<long long> d_replies;
+  GBuf<GOp> d_pop;
 
   ~cl_graph() {
     if (!dev_ready) return;
@@ -191,6 +202,9 @@ struct cl_graph {
     d_chin.release(); d_fifo.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
     d_sched.release(); d_scratch.release(); d_big.release(); d_cpart.release();
     d_trace.release(); d_trace_cnt.release();
+    d_outbox.release(); d_inbox.release(); d_out_n.release(); d_rmlist.release(); d_reports.release();
+    d_rep_in.release(); d_trigv.release(); d_s0.release(); d_rdraw.release(); d_draw0.release();
+    d_replies.release(); d_pop.release();
     for (auto& ev : ev_pool) {
       (void)hipEventDestroy(ev.first);
       (void)hipEventDestroy(ev.second);
@@ -508,6 +522,17 @@ struct cl_graph {
     p.trace = trace_cap > 0 ? d_trace.p : nullptr;
     p.trace_cnt = trace_cap > 0 ? d_trace_cnt.p : nullptr;
     p.trace_cap = trace_cap;
+    p.part = part ? 1 : 0;
+    p.part_lo = part ? part_lo : 0;
+    p.part_hi = part ? part_hi : n;
+    p.blk_lo = p.part_lo / kGThreads;
+    p.blk_hi = (p.part_hi + kGThreads - 1) / kGThreads;
+    p.outbox = d_outbox.p;
+    p.out_n = d_out_n.p;
+    p.rmlist = d_rmlist.p;
+    p.reports = d_reports.p;
+    p.trigv = d_trigv.p;
+    p.rdraw = d_rdraw.p;
   }
 
   int upload_ops() {
@@ -599,6 +624,7 @@ struct cl_graph {
 
   // Execute program ops [executed, end) on the device; from scratch if `fresh`.
   int run(bool fresh) {
+    if (part) return gerr(CL_E_STATE, "a partitioned run advances only through the cl_graph_part_* calls");
     int rc = freeze();
     if (rc) return rc;
     if (n == 0) return gerr(CL_E_STATE, "the topology has no nodes");
@@ -1374,6 +1400,158 @@ int cl_graph_get_checksums(cl_graph* g, int64_t* out) {
   out[CL_GSUM_FINAL_RESIDUAL] = fin < 0 ? -fin : fin;
   out[CL_GSUM_DIGEST] = (int64_t)r[2];
   out[CL_GSUM_IN_FLIGHT] = (int64_t)r[1];
+  return CL_OK;
+}
+
+// ---- graph-partitioned mode ---------------------------------------------
+#define G_PART(g)                                                                            \
+  do {                                                                                       \
+    if (!(g)->part) return gerr(CL_E_STATE, "not a partitioned run (cl_graph_part_begin)");  \
+  } while (0)
+
+int cl_graph_part_begin(cl_graph* g, int32_t node_lo, int32_t node_hi) {
+  G_CHECK(g);
+  int rc = g->freeze();
+  if (rc) return rc;
+  if (g->part) return gerr(CL_E_STATE, "the partitioned run has begun");
+  if (!g->prog.empty()) return gerr(CL_E_STATE, "a partitioned run starts from an empty program");
+  if (g->trace_cap > 0) return gerr(CL_E_STATE, "the event trace is not available in the partitioned mode");
+  if (g->go_seed) return gerr(CL_E_STATE, "the partitioned mode takes the counter hash or an explicit delay schedule");
+  if (node_lo < 0 || node_lo > node_hi || node_hi > g->n || node_lo % kGThreads ||
+      (node_hi != g->n && node_hi % kGThreads))
+    return gerr(CL_E_INVALID, "node range [%d, %d) must be block-aligned (%d) within [0, %d)", node_lo, node_hi,
+                kGThreads, g->n);
+  if ((rc = g->ensure_device())) return rc;
+  GHIP(hipSetDevice(g->device));
+  bool realloc = false;
+  if ((rc = g->ensure_state(&realloc)) || (rc = g->ensure_sched()) || (rc = g->upload_ops())) return rc;
+  const size_t N = (size_t)g->n;
+  if ((rc = g->d_outbox.ensure(N)) || (rc = g->d_out_n.ensure(4)) || (rc = g->d_rmlist.ensure(N)) ||
+      (rc = g->d_reports.ensure(N)) || (rc = g->d_trigv.ensure(N)) || (rc = g->d_rdraw.ensure(N)) ||
+      (rc = g->d_pop.ensure(1)))
+    return rc;
+  g->part = true;
+  g->part_lo = node_lo;
+  g->part_hi = node_hi;
+  g->fill_params();
+  if ((rc = g->k_err(cg_launch_reset(g->P, g->d_init_tok.p, g->stream)))) return rc;
+  GHIP(hipMemsetAsync(g->d_trigv.p, 0, N * sizeof(int32_t), g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  g->time = 0;
+  g->hang = false;
+  g->executed = g->prog.size();
+  g->state_valid = true;
+  return CL_OK;
+}
+
+int cl_graph_part_snapshot(cl_graph* g, int32_t node, int32_t* out_sid) {
+  G_CHECK(g);
+  G_PART(g);
+  if (node < 0 || node >= g->n) return gerr(CL_E_UNKNOWN_NODE, "snapshot at unknown rank %d", node);
+  if (g->n_sids >= g->s_cap) return gerr(CL_E_LIMIT, "more than %d snapshots (cl_graph_set_limits)", g->s_cap);
+  const GOp op{GOP_SNAP, node, g->n_sids, 0};
+  GHIP(hipMemcpy(g->d_pop.p, &op, sizeof op, hipMemcpyHostToDevice));
+  GParams q = g->P;
+  q.ops = g->d_pop.p;
+  int rc = g->k_err(cg_launch_hostops(q, (int32_t)g->time, 0, 1, g->stream));
+  if (rc) return rc;
+  if (out_sid) *out_sid = g->n_sids;
+  g->n_sids++;
+  return CL_OK;
+}
+
+int cl_graph_part_pick(cl_graph* g, int32_t* rows, int64_t cap, int64_t* n_rows) {
+  G_CHECK(g);
+  G_PART(g);
+  if (!n_rows || (cap > 0 && !rows)) return gerr(CL_E_INVALID, "null output");
+  if (g->time + 1 > kMaxGraphTime) return gerr(CL_E_LIMIT, "simulated time would exceed %lld ticks", (long long)kMaxGraphTime);
+  ++g->time;
+  int rc = g->k_err(cg_launch_part_pick(g->P, (int32_t)g->time, g->stream));
+  if (rc) return rc;
+  uint32_t cnt[4];
+  GHIP(hipMemcpyAsync(cnt, g->d_out_n.p, sizeof cnt, hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  *n_rows = cnt[0];
+  if ((int64_t)cnt[0] > cap) return gerr(CL_E_LIMIT, "%u outgoing deliveries exceed cap %lld", cnt[0], (long long)cap);
+  if (cnt[0]) GHIP(hipMemcpy(rows, g->d_outbox.p, cnt[0] * sizeof(PDel), hipMemcpyDeviceToHost));
+  return CL_OK;
+}
+
+int cl_graph_part_receive(cl_graph* g, const int32_t* rows, int64_t n, int32_t* reports, int64_t cap,
+                          int64_t* n_reports) {
+  G_CHECK(g);
+  G_PART(g);
+  if (!n_reports || (n > 0 && !rows) || (cap > 0 && !reports)) return gerr(CL_E_INVALID, "null array");
+  if (n < 0 || n > g->n) return gerr(CL_E_INVALID, "%lld incoming deliveries", (long long)n);
+  int rc = g->d_inbox.ensure((size_t)n);
+  if (rc) return rc;
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t* r = rows + 4 * i;
+    if (r[1] < g->part_lo || r[1] >= g->part_hi || r[0] < 0 || r[0] >= g->n || r[2] < 0 || r[2] >= g->e)
+      return gerr(CL_E_INVALID, "delivery %lld is not addressed to this device's nodes", (long long)i);
+  }
+  if (n) GHIP(hipMemcpyAsync(g->d_inbox.p, rows, (size_t)n * sizeof(PDel), hipMemcpyHostToDevice, g->stream));
+  if ((rc = g->k_err(cg_launch_part_receive(g->P, (int32_t)g->time, g->d_inbox.p, (int32_t)n, g->stream)))) return rc;
+  uint32_t cnt[4];
+  GHIP(hipMemcpyAsync(cnt, g->d_out_n.p, sizeof cnt, hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  *n_reports = cnt[2];
+  if ((int64_t)cnt[2] > cap) return gerr(CL_E_LIMIT, "%u reports exceed cap %lld", cnt[2], (long long)cap);
+  if (cnt[2]) GHIP(hipMemcpy(reports, g->d_reports.p, cnt[2] * sizeof(int2), hipMemcpyDeviceToHost));
+  return CL_OK;
+}
+
+int cl_graph_part_tally(cl_graph* g, int32_t step, const int32_t* reports, int64_t n, int64_t* totals) {
+  G_CHECK(g);
+  G_PART(g);
+  if (!totals || (n > 0 && !reports)) return gerr(CL_E_INVALID, "null array");
+  if (n < 0 || n > g->n) return gerr(CL_E_INVALID, "%lld reports", (long long)n);
+  for (int64_t i = 0; i < n; ++i)
+    if (reports[2 * i] < g->part_lo || reports[2 * i] >= g->part_hi || reports[2 * i + 1] < 0)
+      return gerr(CL_E_INVALID, "report %lld is not about this device's senders", (long long)i);
+  int rc = g->d_rep_in.ensure((size_t)n);
+  if (rc) return rc;
+  if (n) GHIP(hipMemcpyAsync(g->d_rep_in.p, reports, (size_t)n * sizeof(int2), hipMemcpyHostToDevice, g->stream));
+  if ((rc = g->k_err(cg_launch_part_tally(g->P, step, g->d_rep_in.p, (int32_t)n, g->stream)))) return rc;
+  GScal sc;
+  GHIP(hipMemcpyAsync(&sc, g->d_sc.p, sizeof sc, hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  totals[0] = (int64_t)sc.tot_trig;
+  totals[1] = (int64_t)sc.tot_send;
+  return CL_OK;
+}
+
+int cl_graph_part_bases(cl_graph* g, const int64_t* bases, const int32_t* s0, int64_t n, int64_t* draw0) {
+  G_CHECK(g);
+  G_PART(g);
+  if (!bases || (n > 0 && (!s0 || !draw0))) return gerr(CL_E_INVALID, "null array");
+  if (n < 0 || n > g->n) return gerr(CL_E_INVALID, "%lld reports", (long long)n);
+  for (int64_t i = 0; i < n; ++i)
+    if (s0[i] < g->part_lo || s0[i] >= g->part_hi) return gerr(CL_E_INVALID, "sender %d is not this device's", s0[i]);
+  int rc;
+  if ((rc = g->d_s0.ensure((size_t)n)) || (rc = g->d_draw0.ensure((size_t)n))) return rc;
+  if (n) GHIP(hipMemcpyAsync(g->d_s0.p, s0, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, g->stream));
+  if ((rc = g->k_err(cg_launch_part_bases(g->P, bases[0], bases[1], bases[2], bases[3], g->d_s0.p, (int32_t)n,
+                                          g->d_draw0.p, g->stream))))
+    return rc;
+  if (n) GHIP(hipMemcpyAsync(draw0, g->d_draw0.p, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  return CL_OK;
+}
+
+int cl_graph_part_push(cl_graph* g, int32_t step, const int64_t* replies, int64_t n) {
+  G_CHECK(g);
+  G_PART(g);
+  if (n > 0 && !replies) return gerr(CL_E_INVALID, "null array");
+  if (n < 0 || n > g->n) return gerr(CL_E_INVALID, "%lld replies", (long long)n);
+  for (int64_t i = 0; i < n; ++i)
+    if (replies[2 * i] < 0 || replies[2 * i] >= g->n || (replies[2 * i] >= g->part_lo && replies[2 * i] < g->part_hi))
+      return gerr(CL_E_INVALID, "reply %lld names sender %lld", (long long)i, (long long)replies[2 * i]);
+  int rc = g->d_replies.ensure(2 * (size_t)n);
+  if (rc) return rc;
+  if (n) GHIP(hipMemcpyAsync(g->d_replies.p, replies, 2 * (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, g->stream));
+  if ((rc = g->k_err(cg_launch_part_push(g->P, (int32_t)g->time, step, g->d_replies.p, (int32_t)n, g->stream)))) return rc;
+  GHIP(hipStreamSynchronize(g->stream));  // (the staged rows must outlive the launch)
   return CL_OK;
 }
 

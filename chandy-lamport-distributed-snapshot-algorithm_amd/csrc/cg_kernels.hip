@@ -143,7 +143,8 @@ __device__ inline void complete_nodes(const GParams& p, bool done, int32_t sid, 
   const int32_t g = v / kGThreads;
   const int32_t gsize = min(kGThreads, p.n - g * kGThreads);
   if (atomicAdd(&p.gdone[(size_t)sid * p.n_pblocks + g], 1) + 1 != gsize) return;
-  if (atomicAdd(&p.done[sid], 1) + 1 == p.n_pblocks) {
+  // (partitioned mode: this device's groups; the host joins the devices' completions)
+  if (atomicAdd(&p.done[sid], 1) + 1 == p.blk_hi - p.blk_lo) {
     p.ctick[sid] = t;
     ++completed;
   }
@@ -187,15 +188,15 @@ __device__ inline void block_exclusive_scan2(long long& a, long long& b, long lo
 // triggered by v's delivery this tick, and v's traffic send of step `step`.
 // The node's traffic-send bit for the tally (loads issued by the caller at kernel start,
 // ahead of the block's first barrier).
-__device__ inline int32_t tally_send_bit(const GParams& p, int32_t step) {
-  const int v = blockIdx.x * kGThreads + threadIdx.x;
+__device__ inline int32_t tally_send_bit(const GParams& p, int32_t b, int32_t step) {
+  const int v = b * kGThreads + threadIdx.x;
   int32_t j;
   return v < p.n && traffic_send(p, step, v, p.out_off[v + 1] - p.out_off[v], p.tokens[v], &j) ? 1 : 0;
 }
 
-__device__ inline void tally(const GParams& p, int32_t trig, int32_t sendbit) {
+__device__ inline void tally(const GParams& p, int32_t bk, int32_t trig, int32_t sendbit) {
   __shared__ long long sh[2 * (kGThreads / 64)];
-  const int v = blockIdx.x * kGThreads + threadIdx.x;
+  const int v = bk * kGThreads + threadIdx.x;
   long long a = trig, b = sendbit;
   const long long a0 = a, b0 = b;
   long long ta, tb;
@@ -203,8 +204,8 @@ __device__ inline void tally(const GParams& p, int32_t trig, int32_t sendbit) {
   if (a0) p.ltrig[v] = (int32_t)a;
   if (b0) p.lsend[v] = (int32_t)b;
   if (threadIdx.x == 0) {
-    p.bsum[2 * blockIdx.x] = ta;
-    p.bsum[2 * blockIdx.x + 1] = tb;
+    p.bsum[2 * bk] = ta;
+    p.bsum[2 * bk + 1] = tb;
   }
 }
 
@@ -317,9 +318,10 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
   // (blocks of unusually high out-degree) are read from HBM by their sender.
   constexpr int kStage = kGThreads * 12;
   __shared__ uint64_t s_hq[kStage];
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  const int32_t blo = p.out_off[blockIdx.x * kGThreads];
-  const int32_t bhi = p.out_off[min((int)(blockIdx.x + 1) * kGThreads, p.n)];
+  const int bk = p.blk_lo + (int)blockIdx.x;  // (the owned blocks in the partitioned mode)
+  const int s = bk * kGThreads + threadIdx.x;
+  const int32_t blo = p.out_off[bk * kGThreads];
+  const int32_t bhi = p.out_off[min((bk + 1) * kGThreads, p.n)];
   const int32_t nst = min(bhi - blo, kStage);
   int32_t base = 0, od = 0;
   if (s < p.n) {
@@ -345,7 +347,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
     }
   }
   __syncthreads();
-  if (s == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     p.sc->time = t;  // time++ (sim.go:72)
     p.sc->big_n = 0;
   }
@@ -368,6 +370,11 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
       p.hq[ch] = ((uint64_t)(((head + 1) & capm) | (cnt << 16)) << 32) | nrt;
       p.pick[s] = (t << 6) | j;
       const int32_t v = rte.x, k = rte.y;
+      ++c[(pay & kGMarker) ? 2 : 1];
+      if (v < p.part_lo || v >= p.part_hi) {  // partitioned: the receiver's device applies it
+        p.outbox[atomicAdd(&p.out_n[0], 1u)] = PDel{s, v, k, pay};
+        break;
+      }
       ChIn* ci = &p.chin[k];
       ci->tick = (uint32_t)t;
       ci->pay = pay;
@@ -377,8 +384,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
       if (pay & kGMarker) {
         const int32_t sid = (int32_t)(pay & kGPayload);
         atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + v], ((unsigned long long)t << 32) | (uint32_t)s);
-        p.mlist[blockIdx.x * kGThreads + atomicAdd(&s_m, 1)] = MDel{s, v, k, sid};
-        ++c[2];
+        p.mlist[bk * kGThreads + atomicAdd(&s_m, 1)] = MDel{s, v, k, sid};
       } else {
         atomicAdd(&p.tokens[v], (int32_t)pay);  // HandleToken node.go:175
         const uint32_t tc = ci->tokcnt;
@@ -387,25 +393,32 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
           else set_status(p.sc, kGStatusHistOverflow);
         }
         ci->tokcnt = tc + 1;
-        ++c[1];
       }
       break;
     }
   }
   const int idx[3] = {GC_PEEK, GC_POP_TOK, GC_POP_MK};
   block_count<3>(p, idx, c);
-  if (threadIdx.x == 0) p.mcnt[blockIdx.x] = s_m;
+  if (threadIdx.x == 0) p.mcnt[bk] = s_m;
 }
 
 // ---------------------------------------------------------------------------
 // tick phase B: the markers delivered by pick block b's senders, and block b's tally
 // ---------------------------------------------------------------------------
+// REMOTE (partitioned mode): the markers other devices' senders delivered to owned
+// receivers (k_part_apply's rmlist), 256 per block; their broadcast triggers are reported
+// to the senders' devices.  In the partitioned mode the tally runs after that exchange
+// (k_tally), so k_marker only records the triggers.
+template <bool REMOTE>
 __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;
+  const int bk = REMOTE ? (int)blockIdx.x : p.blk_lo + (int)blockIdx.x;
+  const MDel* list = REMOTE ? p.rmlist + (size_t)bk * kGThreads : p.mlist + (size_t)bk * kGThreads;
   // the tally's inputs (node tokens after this tick's deliveries, out-degree) and the
   // block's marker count are loaded while the status check is in flight
-  const int32_t sendbit = tally_send_bit(p, t);
-  const int nm = p.mcnt[blockIdx.x];
+  const int32_t sendbit = p.part ? 0 : tally_send_bit(p, bk, t);
+  const int nm = REMOTE ? min(kGThreads, (int)p.out_n[1] - bk * kGThreads) : p.mcnt[bk];
+  if (REMOTE && nm <= 0) return;
   if (block_frozen(p)) return;
   __shared__ int s_nb, s_base;
   __shared__ int s_trig[kGThreads];
@@ -426,7 +439,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   int bslot = -1, cslot = -1;
   BigX bx;
   if ((int)threadIdx.x < nm) {
-    const MDel m = p.mlist[blockIdx.x * kGThreads + threadIdx.x];
+    const MDel m = list[threadIdx.x];
     const int32_t s0 = m.s0, v = m.v, k = m.k;
     sid = m.sid;
     vdone = v;
@@ -435,7 +448,10 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
     const int32_t lo = p.in_off[v], hi = p.in_off[v + 1];
     if (key == (((uint64_t)t << 32) | (uint32_t)s0)) {
       // first marker: CreateLocalSnapshot(src) + SendToNeighbors (node.go:153-156)
-      s_trig[s0 - blockIdx.x * kGThreads] = p.out_off[v + 1] - p.out_off[v];
+      const int32_t od = p.out_off[v + 1] - p.out_off[v];
+      if (!p.part) s_trig[s0 - bk * kGThreads] = od;
+      else if (s0 >= p.part_lo && s0 < p.part_hi) p.trigv[s0] = od;  // (one delivery per sender and tick)
+      else p.reports[atomicAdd(&p.out_n[2], 1u)] = make_int2(s0, od);
       if (p.trace)  // SendToNeighbors' SentMsgRecords (node.go:100)
         for (int32_t j = p.out_off[v]; j < p.out_off[v + 1]; ++j)
           gtrace(p, t, kTrTick, (uint32_t)s0, 1u + (uint32_t)(j - p.out_off[v]), TK_SENT_MARKER, v, p.route[j].x, sid);
@@ -462,7 +478,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
     }
   }
   if (done && p.trace) {  // EndSnapshotRecord (sim.go:127); the host moves it behind the last marker
-    const MDel m = p.mlist[blockIdx.x * kGThreads + threadIdx.x];
+    const MDel m = list[threadIdx.x];
     gtrace(p, t, kTrTick, (uint32_t)m.s0, kTrSubEnd, TK_END, vdone, -1, sid);
   }
   complete_nodes(p, done, sid, vdone, t, c[1]);
@@ -493,15 +509,24 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   __syncthreads();
   if (cslot >= 0) p.stok[(size_t)bx.sid * p.n + bx.v] = p.tokens[bx.v] - s_ctsum[cslot];
   if (threadIdx.x == 0 && s_nb) s_base = atomicAdd(&p.sc->big_n, s_nb);
-  tally(p, s_trig[threadIdx.x], sendbit);  // (has a barrier: s_base is final below)
+  if (!p.part) tally(p, bk, s_trig[threadIdx.x], sendbit);  // (has a barrier: s_base is final below)
+  else __syncthreads();
   if (bslot >= 0) p.big[s_base + bslot] = bx;
 }
 
-// Step-0 traffic tally (before the first tick: no triggers).
+// The tally alone: the step-0 traffic (before the first tick: no triggers), and in the
+// partitioned mode every tick's, with the triggers k_marker and the reports recorded.
 __global__ void __launch_bounds__(kGThreads) k_tally(GParams p, int32_t step) {
-  const int32_t sendbit = tally_send_bit(p, step);
+  const int bk = p.blk_lo + (int)blockIdx.x;
+  const int v = bk * kGThreads + threadIdx.x;
+  const int32_t sendbit = tally_send_bit(p, bk, step);
+  int32_t trig = 0;
+  if (p.part && v < p.n) {
+    trig = p.trigv[v];
+    if (trig) p.trigv[v] = 0;
+  }
   if (block_frozen(p)) return;
-  tally(p, 0, sendbit);
+  tally(p, bk, trig, sendbit);
 }
 
 // phase C: exclusive scan of the block tallies (one workgroup, 4 entries per thread),
@@ -510,11 +535,11 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p) {
   if (block_frozen(p)) return;
   __shared__ long long sh[32];
   long long carry_a = 0, carry_b = 0;
-  for (int c0 = 0; c0 < p.n_pblocks; c0 += 4 * blockDim.x) {
+  for (int c0 = p.blk_lo; c0 < p.blk_hi; c0 += 4 * blockDim.x) {
     const int i0 = c0 + 4 * threadIdx.x;
     long long va[4], vb[4], a = 0, b = 0;
     for (int q = 0; q < 4; ++q) {
-      const bool in = i0 + q < p.n_pblocks;
+      const bool in = i0 + q < p.blk_hi;
       va[q] = in ? p.bsum[2 * (i0 + q)] : 0;
       vb[q] = in ? p.bsum[2 * (i0 + q) + 1] : 0;
       a += va[q];
@@ -525,7 +550,7 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p) {
     a += carry_a;
     b += carry_b;
     for (int q = 0; q < 4; ++q) {
-      if (i0 + q < p.n_pblocks) {
+      if (i0 + q < p.blk_hi) {
         p.bsum[2 * (i0 + q)] = a;
         p.bsum[2 * (i0 + q) + 1] = b;
       }
@@ -535,7 +560,10 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p) {
     carry_a += ta;
     carry_b += tb;
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && p.part) {  // the host joins the devices' totals (k_part_bases)
+    p.sc->tot_trig = (unsigned long long)carry_a;
+    p.sc->tot_send = (unsigned long long)carry_b;
+  } else if (threadIdx.x == 0) {
     const unsigned long long d = p.sc->draw;
     p.sc->base_trig = d;
     p.sc->base_send = d + (unsigned long long)carry_a;
@@ -557,6 +585,7 @@ __device__ inline uint64_t next_creation(const GParams& p, int32_t lo, int ncre,
 // First draw index of the broadcast triggered by sender s0's delivery this tick, and of
 // v's traffic send (the scan kernel's block offsets + block-local prefixes).
 __device__ inline unsigned long long broadcast_draw(const GParams& p, int32_t s0) {
+  if (s0 < p.part_lo || s0 >= p.part_hi) return p.rdraw[s0];  // partitioned: the sender's device replied
   return p.sc->base_trig + (unsigned long long)p.bsum[2 * (s0 / kGThreads)] + (unsigned long long)p.ltrig[s0];
 }
 __device__ inline unsigned long long send_draw(const GParams& p, int32_t v) {
@@ -679,10 +708,10 @@ template <int L>
 __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int32_t sarg) {
   const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;
   const int32_t step = sarg != kTimeFromDevice ? sarg : t;  // the traffic of step t follows tick t
-  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t gid = ((int64_t)p.blk_lo * kGThreads * L) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int v = (int)(gid / L), jl = (int)(gid % L);
   int32_t ob = 0, od = 0, ncre = 0, tok = 0;
-  if (v < p.n) {  // loaded while the status check is in flight
+  if (v < p.part_hi) {  // loaded while the status check is in flight
     ob = p.out_off[v];
     od = p.out_off[v + 1] - ob;
     ncre = p.crn[v];
@@ -690,7 +719,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
   }
   if (block_frozen(p)) return;
   unsigned long long c[2] = {0, 0};  // push, peek
-  if (v < p.n) {
+  if (v < p.part_hi) {
     int32_t tj = -1;
     const bool send = traffic_send(p, step, v, od, tok, &tj);
     if (ncre) {
@@ -787,6 +816,9 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
           }
         }
       }
+    } else if (v < p.part_lo || v >= p.part_hi) {
+      // partitioned: the node's device starts the snapshot; every device counts its draws
+      if (threadIdx.x == 0) p.sc->draw += (unsigned long long)od;
     } else {
       // StartSnapshot (sim.go:105-123 -> node.go:198-212): CreateLocalSnapshot("") records
       // every in-link, then SendToNeighbors
@@ -873,15 +905,73 @@ __global__ void __launch_bounds__(kGThreads) k_sg_apply(GParams p, int32_t time,
 }
 
 // ---------------------------------------------------------------------------
+// graph-partitioned mode: the device halves of the exchange steps
+// ---------------------------------------------------------------------------
+// Deliveries by other devices' senders to owned receivers: k_pick's receiver half
+// (HandleToken node.go:174-185 on the token count and channel cursor; markers keyed and
+// staged for k_marker<true>).  Every channel carries at most one delivery per tick.
+__global__ void __launch_bounds__(kGThreads) k_part_apply(GParams p, int32_t t, const PDel* in, int32_t n_in) {
+  const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
+  if (i >= n_in || p.sc->status) return;
+  const PDel d = in[i];
+  ChIn* ci = &p.chin[d.k];
+  ci->tick = (uint32_t)t;
+  ci->pay = d.pay;
+  if (d.pay & kGMarker) {
+    const int32_t sid = (int32_t)(d.pay & kGPayload);
+    atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + d.v], ((unsigned long long)t << 32) | (uint32_t)d.s);
+    p.rmlist[atomicAdd(&p.out_n[1], 1u)] = MDel{d.s, d.v, d.k, sid};
+  } else {
+    atomicAdd(&p.tokens[d.v], (int32_t)d.pay);
+    const uint32_t tc = ci->tokcnt;
+    if (p.hist) {
+      if (tc < (uint32_t)p.hist) p.histv[(size_t)d.k * p.hist + tc] = d.pay;
+      else set_status(p.sc, kGStatusHistOverflow);
+    }
+    ci->tokcnt = tc + 1;
+  }
+}
+
+// Reports of broadcasts that other devices' receivers created on owned senders' markers.
+__global__ void __launch_bounds__(kGThreads) k_part_trig(GParams p, const int2* rep, int32_t n) {
+  const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
+  if (i < n) p.trigv[rep[i].x] = rep[i].y;
+}
+
+// Global draw bases: the triggers of lower devices' senders draw first, then this
+// device's; the next step's sends likewise after every trigger (sim.go:101 call order).
+__global__ void k_part_bases(GParams p, long long trig_before, long long trig_all, long long send_before,
+                             long long send_all) {
+  const unsigned long long d = p.sc->draw;
+  p.sc->base_trig = d + (unsigned long long)trig_before;
+  p.sc->base_send = d + (unsigned long long)(trig_all + send_before);
+  p.sc->draw = d + (unsigned long long)(trig_all + send_all);
+}
+
+// First draw of the broadcast each reported sender triggered (the replies).
+__global__ void __launch_bounds__(kGThreads) k_part_draws(GParams p, const int32_t* s0, int32_t n,
+                                                          unsigned long long* out) {
+  const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
+  if (i < n) out[i] = broadcast_draw(p, s0[i]);
+}
+
+__global__ void __launch_bounds__(kGThreads) k_part_rdraw(GParams p, const long long* rows, int32_t n) {
+  const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
+  if (i < n) p.rdraw[rows[2 * i]] = (unsigned long long)rows[2 * i + 1];
+}
+
+// ---------------------------------------------------------------------------
 // results
 // ---------------------------------------------------------------------------
 // Recorded copies of channels still recording at the end (HandleToken appended them).
 __global__ void k_finish(GParams p, int32_t n_sids, unsigned long long* out) {
-  const size_t total = (size_t)n_sids * p.n;
+  const size_t span = (size_t)(p.part_hi - p.part_lo);  // owned nodes
+  const size_t total = (size_t)n_sids * span;
   unsigned long long rec = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int32_t sid = (int32_t)(i / p.n), v = (int32_t)(i % p.n);
-    if (p.W[i] == ~0ull || p.cnt[i] == kBig) continue;
+    const int32_t sid = (int32_t)(i / span), v = p.part_lo + (int32_t)(i % span);
+    const size_t sv = (size_t)sid * p.n + v;
+    if (p.W[sv] == ~0ull || p.cnt[sv] == kBig) continue;
     const uint64_t* r = p.rec + (size_t)sid * p.e;
     for (int32_t k = p.in_off[v]; k < p.in_off[v + 1]; ++k) {
       const uint64_t x = r[k];
@@ -903,9 +993,10 @@ __device__ inline long long hist_sum(const GParams& p, int32_t k, uint32_t b, ui
 __global__ void k_checks_state(GParams p, unsigned long long* out) {
   const size_t gt = blockIdx.x * (size_t)blockDim.x + threadIdx.x, gs = (size_t)gridDim.x * blockDim.x;
   unsigned long long fin = 0, infl = 0;
-  for (size_t v = gt; v < (size_t)p.n; v += gs) fin += (unsigned long long)(long long)p.tokens[v];
+  // (partitioned mode: owned nodes and their out-channels)
+  for (size_t v = p.part_lo + gt; v < (size_t)p.part_hi; v += gs) fin += (unsigned long long)(long long)p.tokens[v];
   const uint32_t capm = (1u << p.cap_log2) - 1;
-  for (size_t c = gt; c < (size_t)p.e; c += gs) {
+  for (size_t c = p.out_off[p.part_lo] + gt; c < (size_t)p.out_off[p.part_hi]; c += gs) {
     const uint32_t hc = (uint32_t)(p.hq[c] >> 32);
     for (uint32_t q = 0; q < (hc >> 16); ++q) {
       const uint64_t x = p.fifo[(c << p.cap_log2) + (((hc & 0xffffu) + q) & capm)];
@@ -924,14 +1015,16 @@ __global__ void k_checks_snap(GParams p, int32_t n_sids, unsigned long long* out
     if (p.ctick[sid] < 0) continue;
     unsigned long long cut = 0, dig = 0;
     const int32_t* stok = p.stok + (size_t)sid * p.n;
-    for (size_t v = gt; v < (size_t)p.n; v += gs) {
+    for (size_t v = p.part_lo + gt; v < (size_t)p.part_hi; v += gs) {
       const int32_t st = stok[v];
       dig += mix64(cg_hash(0x5107ull, (uint64_t)sid, (uint64_t)v) ^ (uint64_t)(uint32_t)st);
       cut += (unsigned long long)(long long)st;
     }
     const uint64_t* rec = p.rec + (size_t)sid * p.e;
     for (size_t c = gt; c < (size_t)p.e; c += gs) {
-      const int32_t k = p.route[c].y;
+      const int2 rt = p.route[c];
+      if (rt.x < p.part_lo || rt.x >= p.part_hi) continue;  // (partitioned: channels into owned nodes)
+      const int32_t k = rt.y;
       const uint64_t x = rec[k];
       const uint32_t b = (uint32_t)x, e = (uint32_t)(x >> 32);
       const long long s = hist_sum(p, k, b, e);
@@ -965,14 +1058,18 @@ int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream) {
 // thread per node) push with kPushLanes threads per node; p.push_lanes forces either path
 // (cl_graph_set_push_lanes: the exact-match tests run both on the same graphs).
 constexpr int32_t kLanesBelow = 1 << 18;
-void launch_push(const GParams& p, int32_t t, hipStream_t s) {
+// (over the owned node blocks [blk_lo, blk_hi): all of them outside the partitioned mode)
+void launch_push(const GParams& p, int32_t t, int32_t step, hipStream_t s) {
+  const int32_t nb = p.blk_hi - p.blk_lo;
+  if (nb <= 0) return;
   if (p.push_lanes ? p.push_lanes == kPushLanes : p.n < kLanesBelow) {
-    const int64_t m = (int64_t)p.n * kPushLanes;
-    hipLaunchKernelGGL(k_push<kPushLanes>, dim3((unsigned)((m + kGThreads - 1) / kGThreads)), dim3(kGThreads), 0, s, p, t, t);
+    const int64_t m = (int64_t)(p.part_hi - p.part_lo) * kPushLanes;
+    hipLaunchKernelGGL(k_push<kPushLanes>, dim3((unsigned)((m + kGThreads - 1) / kGThreads)), dim3(kGThreads), 0, s, p, t, step);
   } else {
-    hipLaunchKernelGGL(k_push<1>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t, t);
+    hipLaunchKernelGGL(k_push<1>, dim3(nb), dim3(kGThreads), 0, s, p, t, step);
   }
 }
+void launch_push(const GParams& p, int32_t t, hipStream_t s) { launch_push(p, t, t, s); }
 
 int cg_launch_sends(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -985,7 +1082,7 @@ int cg_launch_sends(const GParams& p, int32_t t, void* stream) {
 int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_pick, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
-  hipLaunchKernelGGL(k_marker, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
+  hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
   launch_push(p, t, s);
   return hipGetLastError();
@@ -1002,7 +1099,7 @@ int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain,
   for (int32_t i = 0; i < ticks; ++i) {
     hipLaunchKernelGGL(k_drain_ctl, dim3(1), dim3(1), 0, s, p, n_before, md);
     hipLaunchKernelGGL(k_pick, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, kTimeFromDevice);
-    hipLaunchKernelGGL(k_marker, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, kTimeFromDevice);
+    hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, kTimeFromDevice);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
     launch_push(p, kTimeFromDevice, s);
   }
@@ -1030,9 +1127,51 @@ int cg_launch_sendgroup(const GParams& p, int32_t time, int32_t op_begin, int32_
   return hipGetLastError();
 }
 
+int cg_launch_part_pick(const GParams& p, int32_t t, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if ((e = hipMemsetAsync(p.out_n, 0, 4 * sizeof(uint32_t), s))) return e;
+  if (p.blk_hi > p.blk_lo) hipLaunchKernelGGL(k_pick, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, t);
+  return hipGetLastError();
+}
+
+int cg_launch_part_receive(const GParams& p, int32_t t, const PDel* in, int32_t n_in, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = (unsigned)((n_in + kGThreads - 1) / kGThreads);
+  if (n_in > 0) hipLaunchKernelGGL(k_part_apply, dim3(g), dim3(kGThreads), 0, s, p, t, in, n_in);
+  if (p.blk_hi > p.blk_lo)
+    hipLaunchKernelGGL(k_marker<false>, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, t);
+  if (n_in > 0) hipLaunchKernelGGL(k_marker<true>, dim3(g), dim3(kGThreads), 0, s, p, t);
+  return hipGetLastError();
+}
+
+int cg_launch_part_tally(const GParams& p, int32_t step, const int2* rep, int32_t n_rep, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n_rep > 0) hipLaunchKernelGGL(k_part_trig, dim3((n_rep + kGThreads - 1) / kGThreads), dim3(kGThreads), 0, s, p, rep, n_rep);
+  if (p.blk_hi > p.blk_lo) hipLaunchKernelGGL(k_tally, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, step);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
+  return hipGetLastError();
+}
+
+int cg_launch_part_bases(const GParams& p, int64_t trig_before, int64_t trig_all, int64_t send_before,
+                         int64_t send_all, const int32_t* s0, int32_t n, unsigned long long* draw0, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_part_bases, dim3(1), dim3(1), 0, s, p, (long long)trig_before, (long long)trig_all,
+                     (long long)send_before, (long long)send_all);
+  if (n > 0) hipLaunchKernelGGL(k_part_draws, dim3((n + kGThreads - 1) / kGThreads), dim3(kGThreads), 0, s, p, s0, n, draw0);
+  return hipGetLastError();
+}
+
+int cg_launch_part_push(const GParams& p, int32_t t, int32_t step, const long long* replies, int32_t n, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n > 0) hipLaunchKernelGGL(k_part_rdraw, dim3((n + kGThreads - 1) / kGThreads), dim3(kGThreads), 0, s, p, replies, n);
+  launch_push(p, t, step, s);
+  return hipGetLastError();
+}
+
 int cg_launch_finish(const GParams& p, int32_t n_sids, unsigned long long* out, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int64_t m = (int64_t)n_sids * p.n;
+  const int64_t m = (int64_t)n_sids * (p.part_hi - p.part_lo);
   const int g = m ? (grid_for(m) < 8192 ? grid_for(m) : 8192) : 1;
   hipLaunchKernelGGL(k_finish, dim3(g), dim3(kThreads), 0, s, p, n_sids, out);
   return hipGetLastError();

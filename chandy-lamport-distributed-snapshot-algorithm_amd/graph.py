@@ -71,6 +71,13 @@ def glib():
             "cl_graph_collect_snapshot": [vp, i32, vp, vp, vp, i64],
             "cl_graph_get_counters": [vp, vp],
             "cl_graph_get_checksums": [vp, vp],
+            "cl_graph_part_begin": [vp, i32, i32],
+            "cl_graph_part_snapshot": [vp, i32, vp],
+            "cl_graph_part_pick": [vp, vp, i64, vp],
+            "cl_graph_part_receive": [vp, vp, i64, vp, i64, vp],
+            "cl_graph_part_tally": [vp, i32, vp, i64, vp],
+            "cl_graph_part_bases": [vp, vp, vp, i64, vp],
+            "cl_graph_part_push": [vp, i32, vp, i64],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -320,3 +327,159 @@ class GraphSim:
     def pretty_print(self):
         """Logger.PrettyPrint (logger.go:55-64) as text."""
         return format_log(self.node_ids(), self.trace())
+
+
+class PartitionedGraphSim:
+    """ONE simulation over a graph split into contiguous node-rank ranges, one range per
+    process / GPU (graph-partitioned mode, DESIGN.md §11, include/clgraph.h
+    cl_graph_part_*).  Every rank builds the same topology and program; per tick the
+    ranks exchange deliveries, broadcast-trigger reports, trigger totals and draw replies
+    with dist.exchange_rows / allgather_ints (RCCL over xGMI with exchange_device="cuda",
+    gloo on host tensors).  Results are gathered on every rank: the run equals the
+    whole-graph engine's and the oracle's bit for bit (tests/test_partition_gpu.py).
+
+    There is no reference counterpart (the reference runs one process); the exchange
+    steps restate the tick of sim.go:71-95 across ranks (tests/partition_model.py is the
+    same protocol on the CPU)."""
+
+    def __init__(self, sim, rank, world, exchange_device="cpu"):
+        from . import dist as D
+        self.D, self.g, self.rank, self.world = D, sim, rank, world
+        self.dev = exchange_device
+        n = sim.num_nodes
+        blocks = -(-n // 256)
+        per = -(-blocks // world)
+        self.span = per * 256                    # node ranks per rank, block-aligned
+        self.lo, self.hi = min(n, rank * self.span), min(n, (rank + 1) * self.span)
+        if self.lo >= self.hi:
+            raise ValueError(f"{world} ranks over {blocks} node blocks of 256: rank {rank} would own no nodes")
+        self.n = n
+        self._L = sim._L
+        _check(self._L.cl_graph_part_begin(sim._h, self.lo, self.hi))
+        self.time = 0
+        self.n_sids = 0
+
+    def owner(self, v):
+        return np.asarray(v) // self.span
+
+    def _by_owner(self, rows, col):
+        if len(rows) == 0:
+            return [np.zeros((0, rows.shape[1] if rows.ndim == 2 else 1), dtype=np.int64)] * self.world
+        own = self.owner(rows[:, col])
+        return [rows[own == r].astype(np.int64) for r in range(self.world)]
+
+    def _finish_step(self, step, reports_by_src):
+        """tally -> allgather totals -> bases -> replies -> push (the end of a tick, and the
+        step-0 traffic with no reports)."""
+        mine = np.concatenate([r for r in reports_by_src if len(r)] or [np.zeros((0, 2), dtype=np.int64)])
+        rep = np.ascontiguousarray(mine, dtype=np.int32)
+        tot = np.zeros(2, dtype=np.int64)
+        _check(self._L.cl_graph_part_tally(self.g._h, step, _p(rep), len(rep), _p(tot)))
+        allt = self.D.allgather_ints(tot.tolist(), self.dev)
+        r = self.rank
+        bases = np.array([allt[:r, 0].sum(), allt[:, 0].sum(), allt[:r, 1].sum(), allt[:, 1].sum()], dtype=np.int64)
+        s0 = np.ascontiguousarray(rep[:, 0]) if len(rep) else np.zeros(0, dtype=np.int32)
+        draw0 = np.zeros(max(len(s0), 1), dtype=np.int64)
+        _check(self._L.cl_graph_part_bases(self.g._h, _p(bases), _p(s0), len(s0), _p(draw0)))
+        replies, o = [], 0
+        for src_rows in reports_by_src:            # back to the ranks that reported them
+            k = len(src_rows)
+            replies.append(np.stack([s0[o:o + k].astype(np.int64), draw0[o:o + k]], axis=1) if k
+                           else np.zeros((0, 2), dtype=np.int64))
+            o += k
+        back = self.D.exchange_rows(replies, 2, self.dev)
+        rows = np.ascontiguousarray(np.concatenate([b for b in back if len(b)] or [np.zeros((0, 2), dtype=np.int64)]),
+                                    dtype=np.int64)
+        _check(self._L.cl_graph_part_push(self.g._h, step, _p(rows), len(rows)))
+
+    def start(self):
+        """The step-0 traffic (the whole-graph engine runs it at reset)."""
+        self._finish_step(0, [np.zeros((0, 2), dtype=np.int64)] * self.world)
+
+    def start_snapshot_rank(self, node):            # sim.go:105 (called on every rank)
+        sid = C.c_int32(-1)
+        _check(self._L.cl_graph_part_snapshot(self.g._h, node, C.byref(sid)))
+        self.n_sids += 1
+        return sid.value
+
+    def tick(self):                                 # sim.go:71-95 across the ranks
+        h = self.g._h
+        out = np.zeros((max(self.hi - self.lo, 1), 4), dtype=np.int32)
+        m = C.c_int64(0)
+        _check(self._L.cl_graph_part_pick(h, _p(out), out.shape[0], C.byref(m)))
+        self.time += 1
+        inbox = self.D.exchange_rows(self._by_owner(out[:m.value], 1), 4, self.dev)
+        rows = np.ascontiguousarray(np.concatenate([b for b in inbox if len(b)] or [np.zeros((0, 4), dtype=np.int64)]),
+                                    dtype=np.int32)
+        reps = np.zeros((max(len(rows), 1), 2), dtype=np.int32)
+        q = C.c_int64(0)
+        _check(self._L.cl_graph_part_receive(h, _p(rows), len(rows), _p(reps), reps.shape[0], C.byref(q)))
+        got = self.D.exchange_rows(self._by_owner(reps[:q.value], 0), 2, self.dev)
+        self._finish_step(self.time, got)
+
+    def run_program(self, steps, snap_step=(), snap_rank=()):
+        """The synthetic program: for step k, snapshots scheduled at k,
+        one tick (whose end pushes the traffic of step k + 1)."""
+        self.start()
+        si = 0
+        for k in range(steps):
+            while si < len(snap_step) and snap_step[si] == k:
+                self.start_snapshot_rank(int(snap_rank[si]))
+                si += 1
+            self.tick()
+
+    def completion_ticks(self):
+        """Global completion tick of each snapshot (-1 if some rank's nodes are not all done):
+        the latest of the ranks' local completion ticks."""
+        loc = [self.g.snapshot_tick(s) for s in range(self.n_sids)]
+        allc = self.D.allgather_ints(loc or [0], self.dev)[:, :len(loc)]
+        return [int(allc[:, s].max()) if (allc[:, s] >= 0).all() else -1 for s in range(len(loc))]
+
+    def drain(self, max_ticks=10000):
+        """test_common.go:123-137 across the ranks: tick until every snapshot started so far
+        has completed on every rank, then maxDelay + 1 more ticks."""
+        for _ in range(max_ticks + 1):
+            if all(x >= 0 for x in self.completion_ticks()):
+                for _ in range(6):
+                    self.tick()
+                return True
+            self.tick()
+        return False
+
+    def results(self):
+        """(status, final tokens[n], completion ticks, counters, {sid: (tokens[n], offsets,
+        payloads)} for completed snapshots), gathered on every rank."""
+        import torch.distributed as dist
+        g = self.g
+        cnt = g.counters()
+        st = g.status()
+        tok = g.node_tokens_array()[self.lo:self.hi]
+        ct = self.completion_ticks()
+        src, dst = g.channels()
+        mine = (dst >= self.lo) & (dst < self.hi)
+        snaps = {}
+        for sid, c in enumerate(ct):
+            if c < 0:
+                continue
+            t, off, msg = g.collect_arrays(sid)
+            per = [msg[off[k]:off[k + 1]] for k in np.nonzero(mine)[0]]
+            snaps[sid] = (t[self.lo:self.hi], np.nonzero(mine)[0], per)
+        allr = [None] * self.world
+        dist.all_gather_object(allr, (st, tok, cnt, snaps))
+        status = max(r[0] for r in allr)
+        tokens = np.concatenate([r[1] for r in allr])
+        counters = {k: sum(r[2][k] for r in allr) for k in ("push", "peek", "pop_tok", "pop_mk", "recorded")}
+        counters["completed"] = sum(1 for x in ct if x >= 0)
+        out = {}
+        e = len(src)
+        for sid in snaps:
+            stok = np.concatenate([r[3][sid][0] for r in allr])
+            lists = [None] * e
+            for r in allr:
+                for c, m in zip(r[3][sid][1], r[3][sid][2]):
+                    lists[c] = m
+            off = np.zeros(e + 1, dtype=np.int64)
+            off[1:] = np.cumsum([len(x) for x in lists])
+            vals = np.concatenate(lists) if e else np.zeros(0, dtype=np.int64)
+            out[sid] = (stok, off, vals)
+        return status, tokens, ct, counters, out

@@ -154,6 +154,38 @@ int cl_graph_trace_enable(cl_graph* g, int32_t capacity);
  * LogEvent.nodeTokens.  *n_events = total; CL_E_LIMIT if the run overflowed the capacity. */
 int cl_graph_trace_read(cl_graph* g, cl_log_event* out, int32_t cap, int32_t* n_events);
 
+/* ---- graph-partitioned mode --------------------------
+ * ONE simulation whose nodes are split into contiguous rank ranges over several devices
+ * (one process per GPU).  Each device holds the graph-sized arrays but owns the tokens,
+ * out-channel FIFOs and local snapshots of its nodes [node_lo, node_hi).  There is no
+ * reference interface for this (the reference is one process); the caller moves the rows
+ * between devices (graph.py PartitionedGraphSim over torch.distributed all-to-all).  One
+ * tick:
+ *   part_pick     time++, every owned sender pops its first due head (sim.go:71-95);
+ *                 returns the deliveries to other devices' receivers, rows (s, v, k, pay).
+ *   part_receive  applies the deliveries addressed here (every device's rows for its
+ *                 nodes, any order), handles the markers (node.go:149-171); returns the
+ *                 broadcast triggers of other devices' senders, rows (s0, outdeg).
+ *   part_tally    applies the reports addressed here, tallies triggers and next-step sends
+ *                 of the owned senders; totals[0..1] = (trigger draws, send draws).
+ *   part_bases    bases[4] = (trigger draws of lower devices, of all, send draws of lower
+ *                 devices, of all); returns the first draw of each reported sender s0.
+ *   part_push     replies (s0, draw0) for broadcasts triggered by other devices' senders;
+ *                 pushes broadcasts and traffic sends of step `step` (queue.go:18-20).
+ * The step-0 traffic is part_tally(0) + part_bases + part_push(0) with no rows.
+ * part_snapshot(node) must be called on every device (each counts the draws).  Queries
+ * (node tokens, counters, snapshot ticks, collect) return this device's part: its nodes,
+ * the channels into them, completion over its nodes; the program calls (tick, send,
+ * flush of a program) return CL_E_STATE once the partitioned run began. */
+int cl_graph_part_begin(cl_graph* g, int32_t node_lo, int32_t node_hi);
+int cl_graph_part_snapshot(cl_graph* g, int32_t node, int32_t* out_sid);
+int cl_graph_part_pick(cl_graph* g, int32_t* rows, int64_t cap, int64_t* n_rows);
+int cl_graph_part_receive(cl_graph* g, const int32_t* rows, int64_t n, int32_t* reports, int64_t cap,
+                          int64_t* n_reports);
+int cl_graph_part_tally(cl_graph* g, int32_t step, const int32_t* reports, int64_t n, int64_t* totals);
+int cl_graph_part_bases(cl_graph* g, const int64_t* bases, const int32_t* s0, int64_t n, int64_t* draw0);
+int cl_graph_part_push(cl_graph* g, int32_t step, const int64_t* replies, int64_t n);
+
 /* ---- counter hash of the synthetic workloads ------------------------------------ */
 uint64_t cl_counter_hash(uint64_t seed, uint64_t a, uint64_t b);
 

@@ -220,3 +220,33 @@ def test_streaming_topology_parse_reports_first_error_in_file_order():
     with pytest.raises(cl.ClSnapError) as e:
         g.read_topology_text("\n".join(b))
     assert e.value.code == -4 and "Expected 2 tokens" in str(e.value)
+
+
+def test_partitioned_mode_argument_checks():
+    """cl_graph_part_begin validates the node range and the run before touching a device;
+    PartitionedGraphSim refuses ranks that would own no node block."""
+    import ctypes as C
+    src, dst = G.regular_graph(1000, 4, 1)
+    L = clg.glib()
+
+    def fresh(**kw):
+        g = clg.GraphSim()
+        g.set_topology(np.full(1000, 5), src, dst)
+        return g
+    g = fresh()
+    for lo, hi in ((0, 300), (100, 1000), (512, 256), (-256, 0), (0, 1024)):
+        assert L.cl_graph_part_begin(g._h, lo, hi) == -1, (lo, hi)   # CL_E_INVALID
+    g.Tick(1)
+    assert L.cl_graph_part_begin(g._h, 0, 1000) == -8                # a program exists: CL_E_STATE
+    g = fresh()
+    g.set_delay_go_seed(7)
+    assert L.cl_graph_part_begin(g._h, 0, 1000) == -8                # Go streams are per-process
+    g = fresh()
+    g.trace_enable(16)
+    assert L.cl_graph_part_begin(g._h, 0, 512) == -8
+    g = fresh()
+    assert L.cl_graph_part_pick(g._h, None, 0, C.byref(C.c_int64())) == -8   # not partitioned
+    with pytest.raises(cl.ClSnapError):
+        clg.PartitionedGraphSim(fresh(), 3, 4)        # a valid range: fails loudly without a GPU
+    with pytest.raises(ValueError):
+        clg.PartitionedGraphSim(fresh(), 2, 3)        # 4 blocks over 3 ranks: 2 + 2 + 0
