@@ -162,10 +162,6 @@ struct GParams {
   // [e] lo32: receiveTime of the head packet (kEmpty if the queue is empty),
   //     hi32: ring head (lo16) | packets queued (hi16)
   uint64_t* hq;
-  // per sender [n]: the earliest head receiveTime over its non-empty out-channels (kEmpty:
-  // none) and their count -- k_pick skips the head scan of a sender with nothing due
-  uint32_t* sdue;
-  uint32_t* snne;
   uint64_t* fifo;      // [e << cap_log2]
   ChIn* chin;          // [e] by in-position
   uint32_t* histv;     // [e * hist] by in-position

@@ -167,7 +167,6 @@ struct cl_graph {
   GBuf<long long> d_bsum;
   GBuf<uint32_t> d_histv;
   GBuf<uint64_t> d_hq;
-  GBuf<uint32_t> d_sdue, d_snne;
   GBuf<uint64_t> d_fifo, d_W, d_rec;
   GBuf<int32_t> d_cnt, d_stok, d_done, d_ctick;
   GBuf<GScal> d_sc;
@@ -199,7 +198,7 @@ struct cl_graph {
                              &d_pick,    &d_ltrig,  &d_lsend,    &d_crn,    &d_mcnt,   &d_cnt,      &d_stok,
                              &d_done,    &d_ctick};
     for (auto* b : i32s) b->release();
-    d_cre.release(); d_bsum.release(); d_hq.release(); d_sdue.release(); d_snne.release(); d_histv.release(); d_mlist.release(); d_route.release();
+    d_cre.release(); d_bsum.release(); d_hq.release(); d_histv.release(); d_mlist.release(); d_route.release();
     d_chin.release(); d_fifo.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
     d_sched.release(); d_scratch.release(); d_big.release(); d_cpart.release();
     d_trace.release(); d_trace_cnt.release();
@@ -447,7 +446,6 @@ struct cl_graph {
         (rc = d_lsend.ensure(N)) || (rc = d_crn.ensure(N)) || (rc = d_mlist.ensure(NP * kGThreads)) ||
         (rc = d_mcnt.ensure(NP)) || (rc = d_big.ensure(N)) || (rc = d_cpart.ensure((size_t)kParts * kNumCnt)) ||
         (rc = d_cre.ensure(E)) || (rc = d_bsum.ensure(2 * NP)) || (rc = d_hq.ensure(E)) ||
-        (rc = d_sdue.ensure(N)) || (rc = d_snne.ensure(N)) ||
         (rc = d_chin.ensure(E)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
         (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_W.ensure(s_cap * N)) ||
         (rc = d_rec.ensure(s_cap * E)) || (rc = d_cnt.ensure(s_cap * N)) || (rc = d_stok.ensure(s_cap * N)) ||
@@ -509,8 +507,6 @@ struct cl_graph {
     p.big = d_big.p;
     p.cpart = d_cpart.p;
     p.hq = d_hq.p;
-    p.sdue = d_sdue.p;
-    p.snne = d_snne.p;
     p.fifo = d_fifo.p;
     p.chin = d_chin.p;
     p.histv = d_histv.p;
@@ -1195,7 +1191,7 @@ int cl_graph_device_bytes(cl_graph* g, int64_t* bytes) {
        g->d_in_src.bytes() + g->d_init_tok.bytes() + g->d_tokens.bytes() + g->d_pick.bytes() + g->d_chin.bytes() +
        g->d_ltrig.bytes() + g->d_lsend.bytes() + g->d_crn.bytes() + g->d_mlist.bytes() + g->d_mcnt.bytes() +
        g->d_big.bytes() + g->d_cpart.bytes() +
-       g->d_cre.bytes() + g->d_bsum.bytes() + g->d_hq.bytes() + g->d_sdue.bytes() + g->d_snne.bytes() +
+       g->d_cre.bytes() + g->d_bsum.bytes() + g->d_hq.bytes() +
        g->d_histv.bytes() + g->d_fifo.bytes() + g->d_W.bytes() + g->d_rec.bytes() +
        g->d_cnt.bytes() + g->d_stok.bytes() + g->d_done.bytes() + g->d_ctick.bytes() + g->d_sched.bytes();
   *bytes = (int64_t)b;

@@ -7,9 +7,7 @@
 //              from tick-start state equal the reference's sequential picks: a push made
 //              during tick t is due at >= t+1 and never changes a non-empty queue's head.
 //              The scan reads only the per-channel head receiveTime words (contiguous per
-//              sender), and only for senders whose due word (earliest head over their
-//              non-empty out-channels, kept exact by every push and pop) is <= t; the
-//              others peek their non-empty count.  The FIFO itself is touched only by the pop.  Tokens are applied at
+//              sender); the FIFO itself is touched only by the pop.  Tokens are applied at
 //              once (HandleToken node.go:174-185 is commutative for the token count;
 //              recording is the channel cursor tokcnt); markers are staged for k_marker.
 //   k_marker   HandleMarker (node.go:149-171): the first marker of snapshot s at node v
@@ -108,8 +106,8 @@ __device__ inline uint32_t receive_time(const GParams& p, uint64_t k, int32_t ti
   return (uint32_t)time + 1u + d;
 }
 
-// Queue.Push (queue.go:18-20) onto channel c of sender v.
-__device__ inline void push_entry(const GParams& p, int32_t v, int32_t c, uint32_t payload, uint32_t rt,
+// Queue.Push (queue.go:18-20) onto channel c.
+__device__ inline void push_entry(const GParams& p, int32_t c, uint32_t payload, uint32_t rt,
                                   unsigned long long& pushes) {
   const uint64_t q = p.hq[c];
   const uint32_t hc = (uint32_t)(q >> 32);
@@ -120,10 +118,6 @@ __device__ inline void push_entry(const GParams& p, int32_t v, int32_t c, uint32
   }
   p.fifo[((size_t)c << p.cap_log2) + ((head + cnt) & (cap - 1))] = ((uint64_t)rt << 32) | payload;
   p.hq[c] = ((uint64_t)(head | ((cnt + 1) << 16)) << 32) | (cnt == 0 ? rt : (uint32_t)q);
-  if (cnt == 0) {  // a new head: the sender's earliest head and non-empty count
-    atomicMin(&p.sdue[v], rt);
-    atomicAdd(&p.snne[v], 1u);
-  }
   ++pushes;
 }
 
@@ -309,10 +303,6 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
     p.chin[i] = ChIn{0u, 0u, 0u, p.in_src[i]};
     p.hq[i] = kEmpty;
   }
-  if (i < (size_t)p.n) {
-    p.sdue[i] = kEmpty;
-    p.snne[i] = 0u;
-  }
   if (i < (size_t)p.s_cap) p.ctick[i] = -1;
 }
 
@@ -322,92 +312,89 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
 __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
   __shared__ int s_m;
   const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;  // drain ticks: set by k_drain_ctl
+  // Head receiveTime words of the block's senders: the block's out-channels are one
+  // contiguous CSR range, loaded once with coalesced loads (a lane-per-sender prefetch
+  // touched 64 separate 64 B segments per wave instruction).  Channels past kStage
+  // (blocks of unusually high out-degree) are read from HBM by their sender.
+  constexpr int kStage = kGThreads * 12;
+  __shared__ uint64_t s_hq[kStage];
   const int bk = p.blk_lo + (int)blockIdx.x;  // (the owned blocks in the partitioned mode)
   const int s = bk * kGThreads + threadIdx.x;
+  const int32_t blo = p.out_off[bk * kGThreads];
+  const int32_t bhi = p.out_off[min((bk + 1) * kGThreads, p.n)];
+  const int32_t nst = min(bhi - blo, kStage);
   int32_t base = 0, od = 0;
-  uint32_t due = kEmpty, nne = 0;
   if (s < p.n) {
     base = p.out_off[s];
     od = p.out_off[s + 1] - base;
-    due = p.sdue[s];
-    nne = p.snne[s];
   }
-  // (the loads above are in flight during the status check: one latency, not two)
+  // (topology loads above are in flight during the status check: one latency, not two)
   if (block_frozen(p)) return;
   if (threadIdx.x == 0) s_m = 0;
+  {
+    // all loads issued before the first LDS store: one HBM latency, not one per stride
+    constexpr int kPer = kStage / kGThreads;
+    uint64_t tmp[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int32_t i = threadIdx.x + k * kGThreads;
+      tmp[k] = i < nst ? p.hq[blo + i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int32_t i = threadIdx.x + k * kGThreads;
+      if (i < nst) s_hq[i] = tmp[k];
+    }
+  }
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     p.sc->time = t;  // time++ (sim.go:72)
     p.sc->big_n = 0;
   }
   unsigned long long c[3] = {0, 0, 0};  // peek, pop_tok, pop_mk
-  if (s < p.n && due > (uint32_t)t) {
-    c[0] += nne;  // nothing due: the scan peeks every non-empty head and pops none (sim.go:82-84)
-  } else if (s < p.n) {
-    // Scan the head receiveTime words in dest order: the first due head is popped; the
-    // earliest head among the others becomes the sender's new due time.  Loads are issued
-    // eight at a time (one 64-byte row of an 8-out node) ahead of their use.
-    int32_t pj = -1;
-    uint64_t pq = 0;
-    uint32_t nd = kEmpty;
-    for (int32_t j0 = 0; j0 < od; j0 += 8) {
-      uint64_t q[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) q[k] = j0 + k < od ? p.hq[base + j0 + k] : (uint64_t)kEmpty;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t rt = (uint32_t)q[k];
-        if (rt == kEmpty) continue;
-        if (pj < 0) {
-          ++c[0];  // Queue.Peek, sim.go:83
-          if (rt <= (uint32_t)t) {
-            pj = j0 + k;
-            pq = q[k];
-            continue;
-          }
-        }
-        nd = min(nd, rt);
-      }
-    }
-    if (pj < 0) {  // (not reached while the due word is exact: keep it so)
-      p.sdue[s] = nd;
-    } else {
-      const int32_t ch = base + pj;
-      const uint32_t hc = (uint32_t)(pq >> 32), capm = (1u << p.cap_log2) - 1;
+  if (s < p.n) {
+    for (int j = 0; j < od; ++j) {
+      const int32_t li = base + j - blo;
+      const uint64_t q = li < kStage ? s_hq[li] : p.hq[base + j];
+      const uint32_t rt = (uint32_t)q;
+      if (rt == kEmpty) continue;
+      ++c[0];  // Queue.Peek, sim.go:83
+      if (rt > (uint32_t)t) continue;
+      const int32_t ch = base + j;
+      const uint32_t hc = (uint32_t)(q >> 32), capm = (1u << p.cap_log2) - 1;
       const uint32_t head = hc & 0xffffu, cnt = (hc >> 16) - 1;
       const size_t ring = (size_t)ch << p.cap_log2;
       const int2 rte = p.route[ch];
       const uint32_t pay = (uint32_t)p.fifo[ring + head];
       const uint32_t nrt = cnt ? (uint32_t)(p.fifo[ring + ((head + 1) & capm)] >> 32) : kEmpty;
       p.hq[ch] = ((uint64_t)(((head + 1) & capm) | (cnt << 16)) << 32) | nrt;
-      p.sdue[s] = min(nd, nrt);
-      if (!cnt) p.snne[s] = nne - 1;
-      p.pick[s] = (t << 6) | pj;
+      p.pick[s] = (t << 6) | j;
       const int32_t v = rte.x, k = rte.y;
       ++c[(pay & kGMarker) ? 2 : 1];
       if (v < p.part_lo || v >= p.part_hi) {  // partitioned: the receiver's device applies it
         p.outbox[atomicAdd(&p.out_n[0], 1u)] = PDel{s, v, k, pay};
-      } else {
-        ChIn* ci = &p.chin[k];
-        ci->tick = (uint32_t)t;
-        ci->pay = pay;
-        // ReceivedMsgRecord (sim.go:86)
-        gtrace(p, t, kTrTick, (uint32_t)s, 0u, (pay & kGMarker) ? TK_RECV_MARKER : TK_RECV_TOKEN, v, s,
-               (int32_t)(pay & kGPayload));
-        if (pay & kGMarker) {
-          const int32_t sid = (int32_t)(pay & kGPayload);
-          atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + v], ((unsigned long long)t << 32) | (uint32_t)s);
-          p.mlist[bk * kGThreads + atomicAdd(&s_m, 1)] = MDel{s, v, k, sid};
-        } else {
-          atomicAdd(&p.tokens[v], (int32_t)pay);  // HandleToken node.go:175
-          const uint32_t tc = ci->tokcnt;
-          if (p.hist) {
-            if (tc < (uint32_t)p.hist) p.histv[(size_t)k * p.hist + tc] = pay;
-            else set_status(p.sc, kGStatusHistOverflow);
-          }
-          ci->tokcnt = tc + 1;
-        }
+        break;
       }
+      ChIn* ci = &p.chin[k];
+      ci->tick = (uint32_t)t;
+      ci->pay = pay;
+      // ReceivedMsgRecord (sim.go:86)
+      gtrace(p, t, kTrTick, (uint32_t)s, 0u, (pay & kGMarker) ? TK_RECV_MARKER : TK_RECV_TOKEN, v, s,
+             (int32_t)(pay & kGPayload));
+      if (pay & kGMarker) {
+        const int32_t sid = (int32_t)(pay & kGPayload);
+        atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + v], ((unsigned long long)t << 32) | (uint32_t)s);
+        p.mlist[bk * kGThreads + atomicAdd(&s_m, 1)] = MDel{s, v, k, sid};
+      } else {
+        atomicAdd(&p.tokens[v], (int32_t)pay);  // HandleToken node.go:175
+        const uint32_t tc = ci->tokcnt;
+        if (p.hist) {
+          if (tc < (uint32_t)p.hist) p.histv[(size_t)k * p.hist + tc] = pay;
+          else set_status(p.sc, kGStatusHistOverflow);
+        }
+        ci->tokcnt = tc + 1;
+      }
+      break;
     }
   }
   const int idx[3] = {GC_PEEK, GC_POP_TOK, GC_POP_MK};
@@ -605,10 +592,9 @@ __device__ inline unsigned long long send_draw(const GParams& p, int32_t v) {
   return p.sc->base_send + (unsigned long long)p.bsum[2 * (v / kGThreads) + 1] + (unsigned long long)p.lsend[v];
 }
 
-// Queue.Push onto a channel whose head word q is held in a register; a new head lowers
-// dmin and counts in dadd (the caller folds them into the sender's due word).
+// Queue.Push onto a channel whose head word q is held in a register.
 __device__ inline void push_q(const GParams& p, int32_t c, uint64_t& q, uint32_t payload, uint32_t rt,
-                              unsigned long long& pushes, uint32_t& dmin, uint32_t& dadd) {
+                              unsigned long long& pushes) {
   const uint32_t hc = (uint32_t)(q >> 32);
   const uint32_t head = hc & 0xffffu, cnt = hc >> 16, cap = 1u << p.cap_log2;
   if (cnt >= cap) {
@@ -617,10 +603,6 @@ __device__ inline void push_q(const GParams& p, int32_t c, uint64_t& q, uint32_t
   }
   p.fifo[((size_t)c << p.cap_log2) + ((head + cnt) & (cap - 1))] = ((uint64_t)rt << 32) | payload;
   q = ((uint64_t)(head | ((cnt + 1) << 16)) << 32) | (cnt == 0 ? rt : (uint32_t)q);
-  if (cnt == 0) {
-    dmin = min(dmin, rt);
-    ++dadd;
-  }
   ++pushes;
 }
 
@@ -636,7 +618,7 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
                                      bool send, int32_t tok, int32_t tj, unsigned long long (&c)[2]) {
   p.crn[v] = 0;
   const int32_t lo = p.in_off[v];
-  uint32_t srt = 0, dmin = kEmpty, dadd = 0;
+  uint32_t srt = 0;
   if (send) {
     // SendTokens(v, out-link tj, 1): node.go:112-131
     p.tokens[v] = tok - 1;
@@ -665,13 +647,13 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
       const unsigned long long draw0 = broadcast_draw(p, s0) + (unsigned long long)j0;
 #pragma unroll
       for (int j = 0; j < R; ++j)
-        if (j < m) push_q(p, obc + j, q[j], kGMarker | sid, receive_time(p, draw0 + j, t), c[0], dmin, dadd);
+        if (j < m) push_q(p, obc + j, q[j], kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
     }
     if (send) {
 #pragma unroll
       for (int j = 0; j < R; ++j)
         if (j0 + j == tj) {
-          push_q(p, obc + j, q[j], 1u, srt, c[0], dmin, dadd);
+          push_q(p, obc + j, q[j], 1u, srt, c[0]);
           gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[obc + j].x, 1);  // node.go:118
         }
     }
@@ -679,10 +661,6 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
     for (int j = 0; j < R; ++j) {
       if (j < m) p.hq[obc + j] = q[j];
     }
-  }
-  if (dadd) {  // (one thread per node: k_pick of this tick already wrote the word)
-    p.sdue[v] = min(p.sdue[v], dmin);
-    p.snne[v] += dadd;
   }
 }
 
@@ -699,7 +677,6 @@ __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, i
     if (send) p.tokens[v] = tok - 1;  // SendTokens(v, out-link tj, 1): node.go:112-131
   }
   const int32_t lo = p.in_off[v];
-  uint32_t dmin = kEmpty, dadd = 0;
   for (int32_t j = jl; j < od; j += L) {
     uint64_t q = p.hq[ob + j];
     uint64_t prev = 0;
@@ -714,18 +691,13 @@ __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, i
         const int pj = (pk >> 6) == t ? (pk & 63) : 64;
         if (j < pj && (uint32_t)q == kEmpty) ++c[1];
       }
-      push_q(p, ob + j, q, kGMarker | sid, receive_time(p, broadcast_draw(p, s0) + (unsigned long long)j, t), c[0],
-             dmin, dadd);
+      push_q(p, ob + j, q, kGMarker | sid, receive_time(p, broadcast_draw(p, s0) + (unsigned long long)j, t), c[0]);
     }
     if (send && j == tj) {
-      push_q(p, ob + j, q, 1u, receive_time(p, send_draw(p, v), t), c[0], dmin, dadd);
+      push_q(p, ob + j, q, 1u, receive_time(p, send_draw(p, v), t), c[0]);
       gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[ob + j].x, 1);  // node.go:118
     }
     p.hq[ob + j] = q;
-  }
-  if (dadd) {
-    atomicMin(&p.sdue[v], dmin);
-    atomicAdd(&p.snne[v], dadd);
   }
 }
 
@@ -756,7 +728,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
     } else if (send && jl == 0) {
       // SendTokens(v, out-link j, 1): node.go:112-131 (one channel: no batching)
       p.tokens[v] = tok - 1;
-      push_entry(p, v, ob + tj, 1u, receive_time(p, send_draw(p, v), t), c[0]);
+      push_entry(p, ob + tj, 1u, receive_time(p, send_draw(p, v), t), c[0]);
       gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[ob + tj].x, 1);  // node.go:118
     }
   }
@@ -840,7 +812,7 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
             set_status(p.sc, ST_FATAL_UNKNOWN_DEST);
           } else {
             const unsigned long long d = p.sc->draw++;
-            push_entry(p, v, obv + lo, (uint32_t)op.n, receive_time(p, d, time), pushes);
+            push_entry(p, obv + lo, (uint32_t)op.n, receive_time(p, d, time), pushes);
           }
         }
       }
@@ -869,7 +841,7 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
       // the broadcast's pushes go to distinct channels: one thread per out-link, draw d + j
       const unsigned long long d = s_draw;
       for (int32_t j = threadIdx.x; j < od; j += blockDim.x)
-        push_entry(p, v, obv + j, kGMarker | (uint32_t)sid, receive_time(p, d + j, time), pushes);
+        push_entry(p, obv + j, kGMarker | (uint32_t)sid, receive_time(p, d + j, time), pushes);
       if (threadIdx.x == 0) p.sc->draw = d + od;
     }
     __syncthreads();
@@ -918,7 +890,7 @@ __global__ void __launch_bounds__(kGThreads) k_sg_apply(GParams p, int32_t time,
     if (i < first) {  // SentMsgRecord (node.go:118), tokens -= n, Queue.Push with draw d0 + i
       gtrace(p, time, kTrHost, (uint32_t)(ob + i), 0u, TK_SENT_TOKEN, op.a, op.b, op.n);
       p.tokens[op.a] -= op.n;
-      push_entry(p, op.a, c, (uint32_t)op.n, receive_time(p, d0 + (unsigned long long)i, time), pushes);
+      push_entry(p, c, (uint32_t)op.n, receive_time(p, d0 + (unsigned long long)i, time), pushes);
     } else if (i == first) {  // the first failure freezes the run exactly where the program does
       if (fail == 1) {
         set_status(p.sc, ST_FATAL_INSUFFICIENT);
