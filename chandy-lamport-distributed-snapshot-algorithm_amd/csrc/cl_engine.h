@@ -125,9 +125,27 @@ struct Layout {
   int32_t shared;
   int32_t wave_words;
   int32_t wpb;  // waves per workgroup: kWavesPerBlock, fewer when that many waves' state exceeds LDS
+  int32_t rw;   // words per node snapshot record (tokens, then one cursor word per in-link; rec_words)
   // state image per instance (words): per node priv + G_NUM, then s_cap done counters + ndone
   int32_t state_words;
 };
+
+// The exec kernel's degree bound for max degree d (cl_kernels.hip launch_exec).
+inline int32_t degree_bound(int32_t d) {
+  int32_t b = d <= 1 ? 1 : d <= 2 ? 2 : d <= 3 ? 3 : 4;
+  while (b < d) b <<= 1;
+  return b;
+}
+// Words per node snapshot record: [tokens, cursor of in-link 0, 1, ...].  Unrolled kernels
+// write a record with one vector store, so it is padded to a power of two (16 B for the
+// degree-3 8nodes topology); the others store word by word into 1 + id words.
+inline int32_t rec_words(int32_t dmax, int32_t id) {
+  const int32_t D = degree_bound(dmax);
+  if (D > kUnrollMaxD) return 1 + id;
+  int32_t r = 1;
+  while (r < 1 + D) r <<= 1;
+  return r;
+}
 
 inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_log2, int32_t ocap_log2,
                           int32_t s_cap, int64_t sched_row = 0, int32_t delay_budget_words = 0) {
@@ -167,6 +185,7 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
     L.shared = L.x_delay_begin;
   }
   L.wave_words = (base + L.shared + 3) / 4 * 4;
+  L.rw = rec_words(od > id ? od : id, id);
   L.state_words = n_nodes * (L.priv + G_NUM) + s_cap + 1;
   return L;
 }
@@ -186,10 +205,12 @@ struct ExecParams {
   // state: [state_words][stride]; regs: [R_NUM][stride]
   uint32_t* state;
   int32_t* regs;
-  // outputs, node/channel index fastest so a wave's stores coalesce:
+  // outputs, node index fastest so a wave's stores coalesce:
   int32_t* fin_tok;    // [stride][N]          final node tokens
-  int32_t* snap_tok;   // [S_cap][stride][N]   tokenMap
-  uint32_t* snap_rec;  // [S_cap][stride][C]   lo16 = begin, hi16 = end (channel token cursor)
+  // [S_cap][stride][N][rw] one record per (snapshot, node), written when the node creates its
+  // local snapshot: word 0 = tokenMap entry, word 1 + k = recording cursors of in-link k
+  // (lo16 = begin, hi16 = end, the end written when the channel's marker arrives)
+  uint32_t* snap_nod;
   int32_t* snap_tick;  // [S_cap][stride]      completion tick or -1
   uint32_t* ovf;       // [C][1 << ocap_log2] spill ring
   uint32_t* ovh;       // [C] spill ring head
@@ -206,8 +227,9 @@ struct SumParams {
   int64_t n_inst, stride;
   const int32_t* regs;
   const int32_t* fin_tok;
-  const int32_t* snap_tok;
-  const uint32_t* snap_rec;
+  int32_t rw;
+  const uint32_t* snap_nod;  // ExecParams::snap_nod
+  const int32_t* ch_slot;    // [C] word of channel c in an instance's records: dest * rw + 1 + in-link
   const int32_t* snap_tick;
   const int32_t* hist_off;  // [C+1] token history of each channel (shared by all instances)
   const int32_t* hist_val;

@@ -256,8 +256,8 @@ struct cl_sim {
   DevBuf<uint8_t> d_sched;
   DevBuf<uint32_t> d_state;
   DevBuf<int32_t> d_regs;
-  DevBuf<int32_t> d_snap_tok;
-  DevBuf<uint32_t> d_snap_rec;
+  DevBuf<uint32_t> d_snap_nod;  // [s_cap][stride][n][lay.rw] node snapshot records
+  DevBuf<int32_t> d_ch_slot;    // [C] word of channel c in an instance's records
   DevBuf<int32_t> d_snap_tick;
   DevBuf<uint32_t> d_ovf;
   DevBuf<uint32_t> d_ovh;
@@ -272,15 +272,15 @@ struct cl_sim {
 
   // host mirrors of results (invalidated by every launch)
   bool h_valid = false;
-  std::vector<int32_t> h_regs, h_snap_tok, h_snap_tick, h_tok;
-  std::vector<uint32_t> h_snap_rec;
+  std::vector<int32_t> h_regs, h_snap_tick, h_tok, ch_slot;
+  std::vector<uint32_t> h_snap_nod;
 
   ~cl_sim() {
     if (dev_ready) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
-      d_snap_tok.release(); d_snap_rec.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
+      d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
       d_ovh.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       for (auto& e : ev_pool) {
@@ -459,7 +459,7 @@ struct cl_sim {
     }
     Layout L = make_layout(n, od, id, cap_log2, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), s_cap,
                            row, kDelayStageWords);
-    if (4ull * s_cap * stride * (uint64_t)std::max(n, std::max(C, 1)) >= (1ull << 32) ||  // byte offsets
+    if (4ull * s_cap * stride * (uint64_t)n * (uint64_t)L.rw >= (1ull << 32) ||  // byte offsets
         (uint64_t)L.state_words * stride >= (1ull << 32))
       return set_err(CL_E_LIMIT, "batch too large for 32-bit output indexing; split it");
     // high-degree topologies: fewer waves per workgroup (one wave's state must fit)
@@ -472,8 +472,12 @@ struct cl_sim {
     if ((rc = d_state.ensure((size_t)lay.state_words * stride))) return rc;
     if ((rc = d_regs.ensure((size_t)R_NUM * stride))) return rc;
     if ((rc = d_fin_tok.ensure((size_t)n * stride))) return rc;
-    if ((rc = d_snap_tok.ensure((size_t)s_cap * n * stride))) return rc;
-    if ((rc = d_snap_rec.ensure((size_t)s_cap * std::max(C, 1) * stride))) return rc;
+    if ((rc = d_snap_nod.ensure((size_t)s_cap * n * lay.rw * stride))) return rc;
+    ch_slot.assign(std::max(C, 1), 0);
+    for (int v = 0; v < n; ++v)
+      for (int k = in_off[v]; k < in_off[v + 1]; ++k) ch_slot[in_ch[k]] = v * lay.rw + 1 + (k - in_off[v]);
+    if ((rc = d_ch_slot.ensure(ch_slot.size()))) return rc;
+    HIP_TRY(hipMemcpy(d_ch_slot.p, ch_slot.data(), ch_slot.size() * 4, hipMemcpyHostToDevice));
     if ((rc = d_snap_tick.ensure((size_t)s_cap * stride))) return rc;
     const size_t ov = lay.ocap_log2 >= 0 ? ((size_t)C << lay.ocap_log2) * stride : 1;
     if ((rc = d_ovf.ensure(ov))) return rc;
@@ -544,8 +548,7 @@ struct cl_sim {
     p.state = d_state.p;
     p.regs = d_regs.p;
     p.fin_tok = d_fin_tok.p;
-    p.snap_tok = d_snap_tok.p;
-    p.snap_rec = d_snap_rec.p;
+    p.snap_nod = d_snap_nod.p;
     p.snap_tick = d_snap_tick.p;
     p.ovf = d_ovf.p;
     p.ovh = d_ovh.p;
@@ -675,20 +678,26 @@ struct cl_sim {
     if (rc) return rc;
     if (h_valid) return CL_OK;
     if (!dev_ready) return set_err(CL_E_STATE, "nothing has run on the device yet");
-    const int n = (int)ids.size(), C = (int)ch_dst.size();
+    const int n = (int)ids.size();
     h_regs.resize((size_t)R_NUM * stride);
-    h_snap_tok.resize((size_t)s_cap * n * stride);
-    h_snap_rec.resize((size_t)s_cap * std::max(C, 1) * stride);
+    h_snap_nod.resize((size_t)s_cap * n * lay.rw * stride);
     h_snap_tick.resize((size_t)s_cap * stride);
     h_tok.resize((size_t)n * stride);
     HIP_TRY(hipMemcpy(h_regs.data(), d_regs.p, h_regs.size() * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(h_snap_tok.data(), d_snap_tok.p, h_snap_tok.size() * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(h_snap_rec.data(), d_snap_rec.p, h_snap_rec.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(h_snap_nod.data(), d_snap_nod.p, h_snap_nod.size() * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(h_snap_tick.data(), d_snap_tick.p, h_snap_tick.size() * 4, hipMemcpyDeviceToHost));
     if (n) HIP_TRY(hipMemcpy(h_tok.data(), d_fin_tok.p, h_tok.size() * 4, hipMemcpyDeviceToHost));
     h_valid = true;
     return CL_OK;
   }
+
+  // Host copies of the node snapshot records (after fetch): tokenMap entry of node v and the
+  // cursor word of channel c in snapshot sid of instance inst.
+  const uint32_t* rec_base(int sid, int64_t inst) const {
+    return &h_snap_nod[((size_t)sid * stride + inst) * ids.size() * lay.rw];
+  }
+  int32_t tok_at(int sid, int64_t inst, int v) const { return (int32_t)rec_base(sid, inst)[(size_t)v * lay.rw]; }
+  uint32_t rec_at(int sid, int64_t inst, int c) const { return rec_base(sid, inst)[ch_slot[c]]; }
 
   int append(Op op) {
     int rc = freeze();
@@ -1046,7 +1055,7 @@ int cl_device_bytes(const cl_sim* sim, int64_t* bytes) {
   SIM_CHECK(sim);
   int64_t b = 0;
   b += sim->d_ops.n * sizeof(Op) + sim->d_topo.n * 4 + sim->d_sched.n + sim->d_state.n * 4 + sim->d_regs.n * 4;
-  b += sim->d_snap_tok.n * 4 + sim->d_snap_rec.n * 4 + sim->d_snap_tick.n * 4 + sim->d_ovf.n * 4;
+  b += sim->d_snap_nod.n * 4 + sim->d_snap_tick.n * 4 + sim->d_ovf.n * 4;
   b += sim->d_ovh.n * 4 + sim->d_hist.n * 4 + sim->d_sums.n * 8 + sim->d_fin_tok.n * 4;
   *bytes = b;
   return CL_OK;
@@ -1099,12 +1108,12 @@ int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens,
   if (sim->h_snap_tick[(size_t)sid * st + inst] < 0)
     return set_err(CL_E_NOT_COMPLETE, "snapshot %d has not completed in instance %lld", sid, (long long)inst);
   const int n = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
-  for (int v = 0; v < n; ++v) tokens[v] = sim->h_snap_tok[((size_t)sid * st + inst) * n + v];
+  for (int v = 0; v < n; ++v) tokens[v] = sim->tok_at(sid, inst, v);
   int64_t m = 0;
   bool fits = true;
   for (int c = 0; c < C; ++c) {
     msg_offsets[c] = m;
-    const uint32_t rec = sim->h_snap_rec[((size_t)sid * st + inst) * C + c];
+    const uint32_t rec = sim->rec_at(sid, inst, c);
     const uint32_t b = rec & 0xffffu, e = rec >> 16;
     for (uint32_t k = b; k < e; ++k, ++m) {
       if (m < msg_cap) msg_tokens[m] = sim->hist[c][k];
@@ -1166,11 +1175,11 @@ int cl_collect_snapshot_range(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t
     const bool done = sim->h_snap_tick[(size_t)sid * st + i] >= 0;
     if (complete) complete[r] = done ? 1 : 0;
     if (tokens)
-      for (int v = 0; v < n; ++v) tokens[r * n + v] = done ? sim->h_snap_tok[((size_t)sid * st + i) * n + v] : -1;
+      for (int v = 0; v < n; ++v) tokens[r * n + v] = done ? sim->tok_at(sid, i, v) : -1;
     for (int c = 0; c < C; ++c) {
       if (msg_offsets) msg_offsets[r * C + c] = m;
       if (!done) continue;
-      const uint32_t rec = sim->h_snap_rec[((size_t)sid * st + i) * C + c];
+      const uint32_t rec = sim->rec_at(sid, i, c);
       const uint32_t b = rec & 0xffffu, e = rec >> 16;
       for (uint32_t k = b; k < e; ++k, ++m) {
         if (m < msg_cap && msg_tokens) msg_tokens[m] = sim->hist[c][k];
@@ -1202,7 +1211,7 @@ int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out) {
     for (int32_t s = 0; s < sim->n_sids; ++s) {
       if (sim->h_snap_tick[(size_t)s * st + i] < 0) continue;
       for (int c = 0; c < C; ++c) {
-        const uint32_t rec = sim->h_snap_rec[((size_t)s * st + i) * C + c];
+        const uint32_t rec = sim->rec_at(s, i, c);
         out[CL_CNT_RECORDED] += (rec >> 16) - (rec & 0xffffu);
       }
     }
@@ -1227,8 +1236,9 @@ int cl_get_checksums(cl_sim* sim, int64_t* out) {
   p.n_inst = sim->n_inst;
   p.stride = sim->stride;
   p.regs = sim->d_regs.p;
-  p.snap_tok = sim->d_snap_tok.p;
-  p.snap_rec = sim->d_snap_rec.p;
+  p.rw = sim->lay.rw;
+  p.snap_nod = sim->d_snap_nod.p;
+  p.ch_slot = sim->d_ch_slot.p;
   p.snap_tick = sim->d_snap_tick.p;
   p.fin_tok = sim->d_fin_tok.p;
   p.hist_off = sim->d_hist.p;

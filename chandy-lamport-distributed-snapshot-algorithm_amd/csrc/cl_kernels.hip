@@ -67,7 +67,7 @@ struct Ctx {
   int32_t indeg, outdeg, out_off;
   // snapshot outputs by 32-bit byte offsets from the (uniform) array bases: the stores use
   // the SGPR-base + 32-bit-VGPR-offset form, with no 64-bit address arithmetic per store
-  uint32_t tok_plane, rec_plane, tick_plane;  // bytes per sid plane (uniform)
+  uint32_t nod_plane, tick_plane;  // bytes per sid plane (uniform)
   bool mul24;  // every plane offset sid * plane fits the 24-bit multiplier
 };
 
@@ -78,11 +78,21 @@ __device__ __forceinline__ uint32_t plane_off(const Ctx& x, uint32_t sid, uint32
 }
 // This lane's byte offsets in snapshot plane 0, recomputed at each store (cheaper than
 // keeping them live in VGPRs through the tick loop).
-__device__ __forceinline__ uint32_t tok_lane(const Ctx& x) { return 4u * (x.inst * (uint32_t)x.p.n_nodes + (uint32_t)x.v); }
-__device__ __forceinline__ uint32_t rec_lane(const Ctx& x) { return 4u * x.inst * (uint32_t)x.p.n_ch; }
+__device__ __forceinline__ uint32_t nod_lane(const Ctx& x) {
+  return 4u * (x.inst * (uint32_t)x.p.n_nodes + (uint32_t)x.v) * (uint32_t)x.lay.rw;
+}
+// CLSNAP_ABL_NOSTORE (diagnostic timing builds only, results invalid): drop the snapshot
+// output stores made during the tick loop, to price them.
+#ifndef CLSNAP_ABL_NOSTORE
+#define CLSNAP_ABL_NOSTORE 0
+#endif
 template <class T>
 __device__ __forceinline__ void st_at(T* base, uint32_t byte_off, T val) {
   *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + byte_off) = val;
+}
+template <class T>
+__device__ __forceinline__ void st_snap(T* base, uint32_t byte_off, T val) {
+  if constexpr (!CLSNAP_ABL_NOSTORE) st_at(base, byte_off, val);
 }
 
 // Append one Logger record (trace build only) for a traced instance.
@@ -207,20 +217,30 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
                                              int32_t arrive) {
   const ExecParams& p = x.p;
   const Layout& lay = x.lay;
-  st_at(p.snap_tok, plane_off(x, (uint32_t)sid, x.tok_plane) + tok_lane(x), ln.tokens);
-  const uint32_t rb = plane_off(x, (uint32_t)sid, x.rec_plane) + rec_lane(x);
+  const uint32_t rb = plane_off(x, (uint32_t)sid, x.nod_plane) + nod_lane(x);
   if constexpr (unrolled(D)) {
+    // the whole record in one vector store (RW words: a power of two, Layout::rw)
+    constexpr int RW = D == 1 ? 2 : D <= 3 ? 4 : 8;
+    uint32_t r[RW];
+    r[0] = (uint32_t)ln.tokens;
 #pragma unroll
-    for (int32_t kj = 0; kj < D; ++kj) {
-      if (kj < x.indeg) {
-        const uint32_t cur = PW(lay.w_cur + kj);
-        st_at(p.snap_rec, rb + ((it[kj] >> 16) << 2), kj == arrive ? (cur | (cur << 16)) : cur);
-      }
+    for (int32_t kj = 0; kj < RW - 1; ++kj) {
+      const uint32_t cur = (kj < D && kj < x.indeg) ? PW(lay.w_cur + kj) : 0u;
+      r[1 + kj] = kj == arrive ? (cur | (cur << 16)) : cur;
+    }
+    (void)it;
+    if constexpr (RW == 2) {
+      st_snap(reinterpret_cast<uint2*>(p.snap_nod), rb, make_uint2(r[0], r[1]));
+    } else {
+#pragma unroll
+      for (int q = 0; q < RW; q += 4)
+        st_snap(reinterpret_cast<uint4*>(p.snap_nod), rb + 4u * q, make_uint4(r[q], r[q + 1], r[q + 2], r[q + 3]));
     }
   } else {
+    st_snap(p.snap_nod, rb, (uint32_t)ln.tokens);
     for (int32_t kj = 0; kj < x.indeg; ++kj) {
       const uint32_t cur = PW(lay.w_cur + kj);
-      st_at(p.snap_rec, rb + ((PW(lay.w_int + kj) >> 16) << 2), kj == arrive ? (cur | (cur << 16)) : cur);
+      st_snap(p.snap_nod, rb + 4u * (1 + kj), kj == arrive ? (cur | (cur << 16)) : cur);
     }
   }
 }
@@ -230,7 +250,7 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
 __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
   const uint32_t old = lds_add(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
   if (old + 1 == (uint32_t)x.p.n_nodes) {
-    st_at(x.p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + 4u * x.inst, ln.time);
+    st_snap(x.p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + 4u * x.inst, ln.time);
     lds_add(&XW(x.lay.x_ndone + x.seg), 1u);
   }
 }
@@ -280,8 +300,8 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
     }
   } else {  // later marker: stop recording this channel
     // hi16 of the cursor word: the channel's end
-    st_at(reinterpret_cast<uint16_t*>(x.p.snap_rec),
-          plane_off(x, (uint32_t)sid, x.rec_plane) + rec_lane(x) + ((w >> 16) << 2) + 2u,
+    st_snap(reinterpret_cast<uint16_t*>(x.p.snap_nod),
+          plane_off(x, (uint32_t)sid, x.nod_plane) + nod_lane(x) + 4u * (1 + (uint32_t)ki) + 2u,
           (uint16_t)PW(lay.w_cur + ki));
     pend = ((pw >> sh) & 0xffu) - 1;
   }
@@ -560,11 +580,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)first * p.sched_row);
     for (uint32_t k = lane; k < words; k += kWave) X[lay.x_delay + k] = src[k];
   }
-  const uint32_t C = (uint32_t)p.n_ch;
   const Ctx x{p, lay, X + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0,
-              4u * st * (uint32_t)N, 4u * st * C, 4u * st,
-              4ull * st * (uint64_t)max(N, (int32_t)C) < (1ull << 24)};
+              4u * st * (uint32_t)N * (uint32_t)lay.rw, 4u * st,
+              4ull * st * (uint64_t)N * (uint64_t)lay.rw < (1ull << 24)};
   InLinks<D> it;
   if constexpr (unrolled(D)) {
 #pragma unroll
@@ -760,6 +779,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
 #undef PW
 #undef XW
 
+#if !defined(CLSNAP_PART) || CLSNAP_PART == 0
 // Per-instance snapshot hash / conservation checks, summed over the batch.
 __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
   const int64_t inst = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -781,13 +801,14 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
       ncomplete++;
       uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)sid;
       int64_t total = 0;
+      const uint32_t* rb = p.snap_nod + ((int64_t)sid * p.stride + inst) * p.n_nodes * p.rw;
       for (int32_t n = 0; n < p.n_nodes; ++n) {
-        const int32_t t = p.snap_tok[((int64_t)sid * p.stride + inst) * p.n_nodes + n];
+        const int32_t t = (int32_t)rb[(int64_t)n * p.rw];
         h = mix64(h ^ (uint64_t)(int64_t)t);
         total += t;
       }
       for (int32_t c = 0; c < p.n_ch; ++c) {
-        const uint32_t rec = p.snap_rec[((int64_t)sid * p.stride + inst) * p.n_ch + c];
+        const uint32_t rec = rb[p.ch_slot[c]];
         const uint32_t b = rec & 0xffffu, e = rec >> 16;
         h = mix64(h ^ ((uint64_t)c << 32) ^ (uint64_t)(e - b));
         const int32_t* hv = p.hist_val + p.hist_off[c];
@@ -811,6 +832,8 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
   for (int k = 0; k < 10; ++k)
     if (v[k]) atomicAdd(&p.out[k], v[k]);
 }
+
+#endif
 
 }  // namespace
 
@@ -838,6 +861,20 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
                            : launch_exec_ds<D, false, false>(p, topo, ops, sched, stream);
 }
 
+// Build split (Makefile): this file is compiled once per degree set so the slow large-D
+// instantiations build in parallel.  CLSNAP_PART 0 holds D <= 4 and the dispatcher, which
+// references the large-D launchers; CLSNAP_PART = D instantiates that D only.  Without
+// CLSNAP_PART one translation unit holds every D up to CLSNAP_MAX_D (variant builds).
+#if defined(CLSNAP_PART) && CLSNAP_PART > 0
+template int launch_exec_d<CLSNAP_PART>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+#else
+#if defined(CLSNAP_PART)
+extern template int launch_exec_d<8>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+extern template int launch_exec_d<16>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+extern template int launch_exec_d<32>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+extern template int launch_exec_d<64>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+extern template int launch_exec_d<128>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+#endif
 // The kernel is instantiated for degree bounds 1, 2, 3, 4, 8, ... CLSNAP_MAX_D.
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
   const int32_t d = p.lay.od > p.lay.id ? p.lay.od : p.lay.id;  // D must bound every in- and out-degree
@@ -872,5 +909,7 @@ int launch_checksums(const SumParams& p, void* stream) {
   hipLaunchKernelGGL(cl_checksum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p);
   return (int)hipGetLastError();
 }
+
+#endif  // CLSNAP_PART
 
 }  // namespace clsnap
