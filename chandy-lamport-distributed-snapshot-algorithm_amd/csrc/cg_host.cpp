@@ -1450,11 +1450,15 @@ int cl_graph_part_snapshot(cl_graph* g, int32_t node, int32_t* out_sid) {
   if (node < 0 || node >= g->n) return gerr(CL_E_UNKNOWN_NODE, "snapshot at unknown rank %d", node);
   if (g->n_sids >= g->s_cap) return gerr(CL_E_LIMIT, "more than %d snapshots (cl_graph_set_limits)", g->s_cap);
   const GOp op{GOP_SNAP, node, g->n_sids, 0};
-  GHIP(hipMemcpy(g->d_pop.p, &op, sizeof op, hipMemcpyHostToDevice));
+  // stream-ordered: a k_hostops of an earlier call may still be queued on g->stream and read
+  // d_pop (a null-stream hipMemcpy does not wait for the non-blocking stream: two snapshots
+  // started back to back raced here)
+  GHIP(hipMemcpyAsync(g->d_pop.p, &op, sizeof op, hipMemcpyHostToDevice, g->stream));
   GParams q = g->P;
   q.ops = g->d_pop.p;
   int rc = g->k_err(cg_launch_hostops(q, (int32_t)g->time, 0, 1, g->stream));
   if (rc) return rc;
+  GHIP(hipStreamSynchronize(g->stream));  // (`op` is a stack copy)
   if (out_sid) *out_sid = g->n_sids;
   g->n_sids++;
   return CL_OK;

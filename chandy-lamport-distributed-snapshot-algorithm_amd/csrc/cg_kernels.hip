@@ -429,6 +429,10 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   __shared__ int32_t s_cpre[kGThreads];
   __shared__ int32_t s_ctsum[kGThreads];
   __shared__ long long s_sh[2 * (kGThreads / 64)];
+  if (!REMOTE && nm == 0 && !p.part) {  // no markers delivered by this block's senders: the tally only
+    tally(p, bk, 0, sendbit);
+    return;
+  }
   s_trig[threadIdx.x] = 0;
   s_ctsum[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_nb = 0;

@@ -150,6 +150,12 @@ inline int32_t rec_words(int32_t dmax, int32_t id) {
 inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_log2, int32_t ocap_log2,
                           int32_t s_cap, int64_t sched_row = 0, int32_t delay_budget_words = 0) {
   Layout L;
+  // unrolled kernels: every lane reserves D out- and in-link words, so the private column
+  // offsets are compile-time constants of (D, cap_log2) in the specialized kernels (ColumnC)
+  const int32_t dmax = od > id ? od : id;
+  const int32_t dbound = degree_bound(dmax);
+  const bool unr = dbound <= kUnrollMaxD;
+  if (unr) od = id = dbound;
   L.cap_log2 = cap_log2;
   L.ocap_log2 = ocap_log2;
   L.od = od;
@@ -163,11 +169,9 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
   L.w_cur = L.w_chw + od;
   L.w_int = L.w_cur + id;
   // in-link words live in registers when the kernel's degree bound is unrolled
-  const int32_t dmax = od > id ? od : id;
-  const int32_t dbound = dmax <= 1 ? 1 : dmax <= 2 ? 2 : dmax <= 4 ? 4 : 8;
-  L.w_pend = L.w_int + (dbound <= kUnrollMaxD ? 0 : id);
-  L.w_trig = L.w_pend + L.sp;
-  L.priv = L.w_trig + id;
+  L.w_trig = L.w_int + (unr ? 0 : id);
+  L.w_pend = L.w_trig + id;
+  L.priv = L.w_pend + L.sp;
   const int32_t base = L.priv * kWave;
   L.x_pick = base;
   L.x_tslot = base + kWave;
@@ -185,10 +189,18 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
     L.shared = L.x_delay_begin;
   }
   L.wave_words = (base + L.shared + 3) / 4 * 4;
-  L.rw = rec_words(od > id ? od : id, id);
+  L.rw = rec_words(dmax, id);
   L.state_words = n_nodes * (L.priv + G_NUM) + s_cap + 1;
   return L;
 }
+
+// The private column of an unrolled kernel with degree bound D and 1 << CAP ring slots
+// (make_layout with od = id = D): compile-time offsets.
+template <int D, int CAP>
+struct ColumnC {
+  static constexpr int32_t w_fifo = 0, w_chw = D << CAP, w_cur = w_chw + D, w_int = w_cur + D, w_trig = w_int,
+                           w_pend = w_trig + D;
+};
 
 // Kernel parameters (passed by value).
 struct ExecParams {

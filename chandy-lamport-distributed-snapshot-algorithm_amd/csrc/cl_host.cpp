@@ -410,6 +410,7 @@ struct cl_sim {
       if (dev_draws >= D) return CL_OK;
       std::vector<uint8_t> sched((size_t)(D * n_inst));
       go_schedule(seed_base, n_inst, D, sched.data());
+      if (dev_ready) HIP_TRY(hipStreamSynchronize(stream));  // (an async launch may read d_sched)
       int rc = d_sched.ensure(sched.size());
       if (rc) return rc;
       HIP_TRY(hipMemcpy(d_sched.p, sched.data(), sched.size(), hipMemcpyHostToDevice));
@@ -422,6 +423,7 @@ struct cl_sim {
     std::vector<uint8_t> padded((size_t)(row * n_inst), 0);
     for (int64_t i = 0; i < n_inst; ++i)
       std::memcpy(&padded[(size_t)(i * row)], &user_sched[(size_t)(i * user_draws)], (size_t)user_draws);
+    if (dev_ready) HIP_TRY(hipStreamSynchronize(stream));  // (an async launch may read d_sched)
     int rc = d_sched.ensure(padded.size());
     if (rc) return rc;
     HIP_TRY(hipMemcpy(d_sched.p, padded.data(), padded.size(), hipMemcpyHostToDevice));
@@ -438,6 +440,7 @@ struct cl_sim {
     if (!need_fresh && lay.wave_words && want_s <= s_cap && ocap <= lay.ocap_log2 && lay.cap_log2 == cap_log2 &&
         layout_row == (go_seeds ? std::max<int64_t>(16, (draws_needed() + 15) / 16 * 16) : (user_draws + 15) / 16 * 16))
       return CL_OK;
+    if (dev_ready) HIP_TRY(hipStreamSynchronize(stream));  // (buffers below may be reallocated or rewritten)
     s_cap = std::max(want_s, s_cap);
     if (s_cap > kMaxSnapshots) return set_err(CL_E_LIMIT, "more than %d snapshots", kMaxSnapshots);
     if (n == 0) return set_err(CL_E_STATE, "the topology has no nodes");
@@ -580,6 +583,9 @@ struct cl_sim {
     int32_t begin = need_fresh ? 0 : executed;
     if (ops.size() != dops_for || begin != dops_begin || !d_ops.p) {
       build_device_program(begin);
+      // an earlier asynchronous launch (cl_rerun) may still read d_ops: a null-stream copy
+      // does not wait for the engine's non-blocking stream
+      HIP_TRY(hipStreamSynchronize(stream));
       if ((rc = d_ops.ensure(std::max<size_t>(dops.size(), 64)))) return rc;
       HIP_TRY(hipMemcpy(d_ops.p, dops.data(), dops.size() * sizeof(Op), hipMemcpyHostToDevice));
       dops_for = ops.size();

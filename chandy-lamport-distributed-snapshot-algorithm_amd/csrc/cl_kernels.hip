@@ -551,12 +551,29 @@ constexpr int waves_for(int D) {
          : (D == 3 || D == 4) ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : 1;
 }
 
-template <int D, bool STAGED, bool TRACE>
+// CAP > 0: the layout's private column is ColumnC<D, CAP> (compile-time offsets: register
+// pressure of the D = 3 kernel 95 VGPRs + 58 SGPR spills -> ~80 VGPRs, no spills); SPILL false
+// compiles out the HBM spill rings (a layout without them).  CAP = 0 reads every offset from
+// the runtime layout (any D, any ring size).
+template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
                                                                          const Op* __restrict__ ops,
                                                                          const uint8_t* __restrict__ sched) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const Layout& lay = p.lay;
+  Layout lay_ = p.lay;
+  if constexpr (CAP > 0) {
+    using Col = ColumnC<D, CAP>;
+    lay_.cap_log2 = CAP;
+    lay_.od = lay_.id = D;
+    lay_.w_fifo = Col::w_fifo;
+    lay_.w_chw = Col::w_chw;
+    lay_.w_cur = Col::w_cur;
+    lay_.w_int = Col::w_int;
+    lay_.w_trig = Col::w_trig;
+    lay_.w_pend = Col::w_pend;
+    if constexpr (!SPILL) lay_.ocap_log2 = -1;
+  }
+  const Layout& lay = lay_;
   const int32_t N = p.n_nodes;
   const int32_t lane = threadIdx.x & (kWave - 1);
   const int32_t wib = threadIdx.x / kWave;
@@ -837,18 +854,18 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
 
 }  // namespace
 
-template <int D, bool STAGED, bool TRACE>
+template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true>
 int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
   const int32_t wpb = p.lay.wpb;
   const size_t lds = (size_t)p.lay.wave_words * wpb * sizeof(uint32_t);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED, TRACE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
   const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
   const unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
-  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE>), dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)stream, p,
+  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL>), dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)stream, p,
                      topo, ops, sched);
   return (int)hipGetLastError();
 }
@@ -857,18 +874,39 @@ template <int D>
 int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
   // The trace build reads delays from HBM (one instantiation per D, debug runs only).
   if (p.trace_n > 0) return launch_exec_ds<D, false, true>(p, topo, ops, sched, stream);
+  if constexpr (unrolled(D)) {
+    // staged delay rows and 2 / 4 / 8 LDS ring slots (every automatic choice): the kernel
+    // specialized on the column layout, with or without HBM spill rings
+    const bool ok = p.lay.od == D && p.lay.id == D;
+    if (p.lay.x_delay > 0 && ok) {
+      const bool sp = p.lay.ocap_log2 >= 0;
+      switch (p.lay.cap_log2) {
+        case 1: return sp ? launch_exec_ds<D, true, false, 1, true>(p, topo, ops, sched, stream)
+                          : launch_exec_ds<D, true, false, 1, false>(p, topo, ops, sched, stream);
+        case 2: return sp ? launch_exec_ds<D, true, false, 2, true>(p, topo, ops, sched, stream)
+                          : launch_exec_ds<D, true, false, 2, false>(p, topo, ops, sched, stream);
+        case 3: return sp ? launch_exec_ds<D, true, false, 3, true>(p, topo, ops, sched, stream)
+                          : launch_exec_ds<D, true, false, 3, false>(p, topo, ops, sched, stream);
+        default: break;
+      }
+    }
+  }
   return p.lay.x_delay > 0 ? launch_exec_ds<D, true, false>(p, topo, ops, sched, stream)
                            : launch_exec_ds<D, false, false>(p, topo, ops, sched, stream);
 }
 
 // Build split (Makefile): this file is compiled once per degree set so the slow large-D
-// instantiations build in parallel.  CLSNAP_PART 0 holds D <= 4 and the dispatcher, which
-// references the large-D launchers; CLSNAP_PART = D instantiates that D only.  Without
+// instantiations build in parallel.  CLSNAP_PART 0 holds the dispatcher and the checksum
+// kernel and references every launcher; CLSNAP_PART = D instantiates that D only.  Without
 // CLSNAP_PART one translation unit holds every D up to CLSNAP_MAX_D (variant builds).
 #if defined(CLSNAP_PART) && CLSNAP_PART > 0
 template int launch_exec_d<CLSNAP_PART>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
 #else
 #if defined(CLSNAP_PART)
+extern template int launch_exec_d<1>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+extern template int launch_exec_d<2>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+extern template int launch_exec_d<3>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+extern template int launch_exec_d<4>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
 extern template int launch_exec_d<8>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
 extern template int launch_exec_d<16>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
 extern template int launch_exec_d<32>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
