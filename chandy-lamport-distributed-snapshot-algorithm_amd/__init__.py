@@ -82,6 +82,7 @@ def lib():
         "cl_synchronize": [vp],
         "cl_last_kernel_ms": [vp, vp],
         "cl_kernel_time": [vp, vp, vp],
+        "cl_replay_spill_free": [vp, vp],
         "cl_num_nodes": [vp, vp],
         "cl_node_id": [vp, i32, vp],
         "cl_num_channels": [vp, vp],
@@ -107,6 +108,8 @@ def lib():
         "cl_trace_read": [vp, i64, vp, i32, vp],
     }
     for name, args in sig.items():
+        if os.environ.get("CLSNAP_VARIANT") and not hasattr(L, name):
+            continue  # (an older diagnostic build: entry points added since are absent)
         f = getattr(L, name)
         f.restype, f.argtypes = C.c_int, args
     L.cl_status_string.restype, L.cl_status_string.argtypes = cp, [i32]
@@ -363,6 +366,12 @@ class ChandyLamportSim:
         ms = C.c_double(0)
         _check(self._L.cl_last_kernel_ms(self._h, C.byref(ms)))
         return ms.value
+
+    def spill_free_replays(self):
+        """True when the next rerun() runs the spill-free kernel (cl_replay_spill_free)."""
+        v = C.c_int32(0)
+        _check(self._L.cl_replay_spill_free(self._h, C.byref(v)))
+        return bool(v.value)
 
     def kernel_time(self):
         """(total exec-kernel ms, launches) since the previous call (HIP events)."""

@@ -106,9 +106,9 @@ enum : int32_t {
   G_TOKENS = 0, G_STARTED, G_TIME, G_DRAW, G_STATUS, G_PEEK, G_POP_TOK, G_POP_MK, G_PUSH, G_NUM
 };
 
-// LDS of one wave: a private column per lane (word k of lane l at lds[k * 64 + l]; a
-// lane only indexes its own column, so every data-dependent access is conflict-free)
-// followed by a small region shared by the wave's lanes.
+// LDS of one wave: a small region shared by the wave's lanes, then a private column per
+// lane (word k of lane l at lds[col + k * 64 + l]; a lane only indexes its own column, so
+// every data-dependent access is conflict-free).
 struct Layout {
   int32_t cap_log2;   // LDS ring slots per out-channel = 1 << cap_log2
   int32_t ocap_log2;  // HBM spill ring per channel = 1 << ocap_log2 (-1 = none)
@@ -123,6 +123,7 @@ struct Layout {
   int32_t x_delay_begin;  // words of the shared region zeroed at start (everything before x_delay)
   int32_t x_delay;        // wave's delay rows staged in LDS (0 = not staged; rows read from HBM)
   int32_t shared;
+  int32_t col;  // first word of the private columns (after the shared region)
   int32_t wave_words;
   int32_t wpb;  // waves per workgroup: kWavesPerBlock, fewer when that many waves' state exceeds LDS
   int32_t rw;   // words per node snapshot record (tokens, then one cursor word per in-link; rec_words)
@@ -172,23 +173,25 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
   L.w_trig = L.w_int + (unr ? 0 : id);
   L.w_pend = L.w_trig + id;
   L.priv = L.w_pend + L.sp;
-  const int32_t base = L.priv * kWave;
-  L.x_pick = base;
-  L.x_tslot = base + kWave;
-  L.x_off = base + 2 * kWave;
-  L.x_done = base + 3 * kWave;
+  // shared region first (its fixed-size arrays at compile-time offsets 0, 64, 128, 192),
+  // then the 64 private columns from word `col`
+  L.x_pick = 0;
+  L.x_tslot = kWave;
+  L.x_off = 2 * kWave;
+  L.x_done = 3 * kWave;
   L.x_ndone = L.x_done + L.ipw * s_cap;
   L.x_acc = L.x_ndone + L.ipw;
-  L.x_delay_begin = L.x_acc + 5 * L.ipw - base;
+  L.x_delay_begin = L.x_acc + 5 * L.ipw;
   const int64_t delay_words = (int64_t)L.ipw * sched_row / 4;  // sched_row is a multiple of 16
   if (sched_row > 0 && delay_words <= delay_budget_words) {
-    L.x_delay = (L.x_acc + 5 * L.ipw + 3) / 4 * 4;  // 16-byte aligned
-    L.shared = L.x_delay + (int32_t)delay_words - base;
+    L.x_delay = (L.x_delay_begin + 3) / 4 * 4;  // 16-byte aligned
+    L.shared = L.x_delay + (int32_t)delay_words;
   } else {
     L.x_delay = 0;
     L.shared = L.x_delay_begin;
   }
-  L.wave_words = (base + L.shared + 3) / 4 * 4;
+  L.col = (L.shared + 3) / 4 * 4;
+  L.wave_words = L.col + L.priv * kWave;
   L.rw = rec_words(dmax, id);
   L.state_words = n_nodes * (L.priv + G_NUM) + s_cap + 1;
   return L;
@@ -226,6 +229,8 @@ struct ExecParams {
   int32_t* snap_tick;  // [S_cap][stride]      completion tick or -1
   uint32_t* ovf;       // [C][1 << ocap_log2] spill ring
   uint32_t* ovh;       // [C] spill ring head
+  uint32_t* spilled;   // set to 1 by any push that went to a spill ring (cl_host: spill-free replays)
+  int32_t nospill;     // this replay is known to fit the LDS rings: run the spill-free kernel
   // event trace of instances [trace_lo, trace_lo + trace_n) (trace kernel build only)
   TraceRec* trace;          // [trace_n][trace_cap]
   uint32_t* trace_cnt;      // [trace_n] records emitted (may exceed trace_cap: overflow)

@@ -261,6 +261,13 @@ struct cl_sim {
   DevBuf<int32_t> d_snap_tick;
   DevBuf<uint32_t> d_ovf;
   DevBuf<uint32_t> d_ovh;
+  DevBuf<uint32_t> d_spilled;  // 1 word: a push of the last spill-capable launch used a spill ring
+  // A fresh full run of ops [0, nospill_ops) with these delays and layout spilled nothing: its
+  // replays (cl_rerun: the same program and delays, hence the same queues) run the
+  // spill-free kernel.  -1: unknown.
+  int64_t nospill_ops = -1;
+  bool spill_probe = false;    // the last launch was a fresh spill-capable full run (of probe_ops ops)
+  int64_t probe_ops = 0;
   DevBuf<int32_t> d_hist;
   DevBuf<unsigned long long> d_sums;
   // device event trace (cl_trace_enable): instances [trace_lo, trace_lo + trace_n)
@@ -281,7 +288,7 @@ struct cl_sim {
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
-      d_ovh.release(); d_hist.release(); d_sums.release();
+      d_ovh.release(); d_spilled.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       for (auto& e : ev_pool) {
         (void)hipEventDestroy(e.first);
@@ -415,6 +422,7 @@ struct cl_sim {
       if (rc) return rc;
       HIP_TRY(hipMemcpy(d_sched.p, sched.data(), sched.size(), hipMemcpyHostToDevice));
       dev_draws = D;  // longer rows of the same streams: saved draw cursors stay valid
+      nospill_ops = -1;
       dev_row = D;
       return CL_OK;
     }
@@ -429,6 +437,7 @@ struct cl_sim {
     HIP_TRY(hipMemcpy(d_sched.p, padded.data(), padded.size(), hipMemcpyHostToDevice));
     dev_draws = user_draws;
     dev_row = row;
+    nospill_ops = -1;
     return CL_OK;
   }
 
@@ -485,6 +494,8 @@ struct cl_sim {
     const size_t ov = lay.ocap_log2 >= 0 ? ((size_t)C << lay.ocap_log2) * stride : 1;
     if ((rc = d_ovf.ensure(ov))) return rc;
     if ((rc = d_ovh.ensure(lay.ocap_log2 >= 0 ? (size_t)std::max(C, 1) * stride : 1))) return rc;
+    if ((rc = d_spilled.ensure(1))) return rc;
+    nospill_ops = -1;  // (a new layout: probe again)
     need_fresh = true;
     return CL_OK;
   }
@@ -555,6 +566,7 @@ struct cl_sim {
     p.snap_tick = d_snap_tick.p;
     p.ovf = d_ovf.p;
     p.ovh = d_ovh.p;
+    p.spilled = d_spilled.p;
     p.ch_dest = d_ch_dest.p;
     if (trace_n > 0) {
       p.trace = d_trace.p;
@@ -602,6 +614,14 @@ struct cl_sim {
     // cl_exec_kernel prologue -- no fill launch before every replay)
     ExecParams p = exec_params(begin, started_before);
     p.save_state = save_state ? 1 : 0;
+    // spill-free replays: a fresh full run whose program and delays already ran once without
+    // touching a spill ring (the same replay fills the same queues)
+    p.nospill = begin == 0 && trace_n == 0 && nospill_ops == (int64_t)ops.size() ? 1 : 0;
+    spill_probe = begin == 0 && trace_n == 0 && !p.nospill && lay.ocap_log2 >= 0;
+    if (spill_probe) {
+      probe_ops = (int64_t)ops.size();
+      HIP_TRY(hipMemsetAsync(d_spilled.p, 0, sizeof(uint32_t), stream));
+    }
     if (ev_used == 256 && (rc = fold_events())) return rc;
     if (ev_used == ev_pool.size()) {
       std::pair<hipEvent_t, hipEvent_t> pr;
@@ -628,6 +648,12 @@ struct cl_sim {
     if (!dev_ready) return CL_OK;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamSynchronize(stream));
+    if (spill_probe) {
+      uint32_t sp = 1;
+      HIP_TRY(hipMemcpy(&sp, d_spilled.p, sizeof sp, hipMemcpyDeviceToHost));
+      if (!sp) nospill_ops = probe_ops;
+      spill_probe = false;
+    }
     return CL_OK;
   }
 
@@ -843,6 +869,7 @@ int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks) 
 
 int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
   SIM_CHECK(sim);
+  sim->nospill_ops = -1;
   sim->go_seeds = true;
   sim->seed_base = seed_base;
   sim->dev_draws = -1;
@@ -852,6 +879,7 @@ int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
 
 int cl_set_delay_schedule(cl_sim* sim, const uint8_t* delays, int64_t draws_per_instance) {
   SIM_CHECK(sim);
+  sim->nospill_ops = -1;
   if (!delays || draws_per_instance <= 0) return set_err(CL_E_INVALID, "empty schedule");
   const size_t n = (size_t)(draws_per_instance * sim->n_inst);
   for (size_t i = 0; i < n; ++i)
@@ -972,6 +1000,15 @@ int cl_flush(cl_sim* sim) {
 int cl_rerun(cl_sim* sim) {
   SIM_CHECK(sim);
   return sim->launch(true, false);
+}
+
+int cl_replay_spill_free(cl_sim* sim, int32_t* on) {
+  SIM_CHECK(sim);
+  if (!on) return set_err(CL_E_INVALID, "null output");
+  int rc = sim->sync();  // (a pending spill probe is read here)
+  if (rc) return rc;
+  *on = sim->lay.ocap_log2 < 0 || sim->nospill_ops == (int64_t)sim->ops.size() ? 1 : 0;
+  return CL_OK;
 }
 
 int cl_synchronize(cl_sim* sim) {

@@ -204,6 +204,7 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
     const uint32_t om = (1u << lay.ocap_log2) - 1;
     const uint32_t h = x.p.ovh[c * x.stride + x.inst];
     x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.stride + x.inst] = e;
+    *x.p.spilled = 1u;  // (a replay of this program needs the spill rings)
   }
   PW(lay.w_chw + ko) = chw + kCountOne;
   ln.push++;
@@ -572,6 +573,10 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     lay_.w_trig = Col::w_trig;
     lay_.w_pend = Col::w_pend;
     if constexpr (!SPILL) lay_.ocap_log2 = -1;
+    lay_.x_pick = 0;
+    lay_.x_tslot = kWave;
+    lay_.x_off = 2 * kWave;
+    lay_.x_done = 3 * kWave;
   }
   const Layout& lay = lay_;
   const int32_t N = p.n_nodes;
@@ -597,7 +602,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)first * p.sched_row);
     for (uint32_t k = lane; k < words; k += kWave) X[lay.x_delay + k] = src[k];
   }
-  const Ctx x{p, lay, X + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
+  const Ctx x{p, lay, X + lay.col + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0,
               4u * st * (uint32_t)N * (uint32_t)lay.rw, 4u * st,
               4ull * st * (uint64_t)N * (uint64_t)lay.rw < (1ull << 24)};
@@ -615,7 +620,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   for (int k = 0; k < 8; ++k) ln.prof[k] = 0;
   const unsigned long long pro0 = PROF_T();
 #endif
-  for (int32_t k = lane; k < lay.x_delay_begin; k += kWave) XW(lay.priv * kWave + k) = 0u;
+  for (int32_t k = lane; k < lay.x_delay_begin; k += kWave) XW(k) = 0u;
   if (p.fresh) {
     // completion ticks start at -1 (no separate fill launch before every replay); the wait
     // orders these stores before any completion store of the same wave
@@ -879,7 +884,7 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
     // specialized on the column layout, with or without HBM spill rings
     const bool ok = p.lay.od == D && p.lay.id == D;
     if (p.lay.x_delay > 0 && ok) {
-      const bool sp = p.lay.ocap_log2 >= 0;
+      const bool sp = p.lay.ocap_log2 >= 0 && !p.nospill;
       switch (p.lay.cap_log2) {
         case 1: return sp ? launch_exec_ds<D, true, false, 1, true>(p, topo, ops, sched, stream)
                           : launch_exec_ds<D, true, false, 1, false>(p, topo, ops, sched, stream);

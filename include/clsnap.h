@@ -141,6 +141,11 @@ int cl_last_kernel_ms(cl_sim* sim, double* ms);
 /* Sum of exec-kernel device times (HIP events around every launch) since the previous
  * call, and the number of launches; resets the accumulator. */
 int cl_kernel_time(cl_sim* sim, double* total_ms, int64_t* launches);
+/* 1 in *on when the next cl_rerun runs the spill-free kernel: a fresh run of the same program
+ * with the same delays and layout already completed without pushing onto an HBM spill ring,
+ * so its replays fill the same LDS queues (engine-internal specialization; results are the
+ * same either way). */
+int cl_replay_spill_free(cl_sim* sim, int32_t* on);
 
 /* ---- topology queries (host only) ---------------------------------------- */
 int cl_num_nodes(const cl_sim* sim, int32_t* n);

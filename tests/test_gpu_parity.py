@@ -249,6 +249,8 @@ def test_rerun_equals_flush_and_oracle(cfg):
     top, events, n, slots = cfg
     sim = engine_run(top, events, n, fifo_lds_slots=slots)
     first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
+    if slots == 2:  # two LDS slots: deep channels must have used the HBM spill rings
+        assert not sim.spill_free_replays()
     _, st, ticks, cnt, hashes = oracle_batch(top, events, n, threads=16)
     want = batch_sums_from_oracle(st, cnt, hashes)
     for r in range(3):
@@ -267,6 +269,42 @@ def test_rerun_equals_flush_and_oracle(cfg):
     for i in np.concatenate([[0, n - 1], rng.choice(n, 24, replace=False)]):
         compare_instance(sim, int(i), oracle_run(top, events, seed=O.REFERENCE_SEED + int(i)),
                          status=status, times=times)
+
+
+def test_spill_free_replay_after_probe():
+    """A flush that never needs an HBM spill ring lets reruns take the spill-free kernel
+    (cl_replay_spill_free); appending events invalidates that until the next full run, and
+    every rerun equals the flush and the oracle."""
+    # A->B carries a send and two markers (depth bound 3 > 2 LDS slots: spill rings are
+    # provisioned), but the ticks between them keep at most one packet queued
+    top = "3\nA 10\nB 10\nC 10\nA B\nB C\nC A\nB A\n"
+    ev = "send A B 2\ntick 6\nsnapshot A\ntick 6\nsnapshot B\n"
+    n = 512
+    sim = cl.ChandyLamportSim(n, fifo_lds_slots=2)
+    sim.read_topology_text(top)
+    sim.read_events_text(ev)
+    sim.flush()
+    first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
+    assert sim.spill_free_replays()
+    for i in range(0, n, 37):
+        compare_instance(sim, i, oracle_run(top, ev, seed=O.REFERENCE_SEED + i), status=first[0], times=first[1])
+    for _ in range(2):
+        sim.rerun()
+        sim.synchronize()
+        assert np.array_equal(sim.status(), first[0]) and np.array_equal(sim.time(), first[1])
+        assert np.array_equal(sim.checksums(), first[2])
+    ev2 = "send A B 1\nsend A B 1\nsend A B 1\nsend A B 1\nsend A B 1\ntick 1\n"
+    sim.read_events_text(ev2)
+    assert not sim.spill_free_replays()  # (the longer program has not run in full yet)
+    sim.rerun()
+    sim.synchronize()
+    ref = cl.ChandyLamportSim(n, fifo_lds_slots=2)  # the same two readEventsFile calls, one flush
+    ref.read_topology_text(top)
+    ref.read_events_text(ev)
+    ref.read_events_text(ev2)
+    ref.flush()
+    assert np.array_equal(sim.status(), ref.status()) and np.array_equal(sim.time(), ref.time())
+    assert np.array_equal(sim.checksums(), ref.checksums())
 
 
 def test_headline_batch_2p20_matches_fixture():
