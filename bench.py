@@ -244,9 +244,10 @@ def main():
                          "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg,
                          "valu": valu,
                          "binding_resource": (
-                             "per-wave issue latency (LDS round trips and dependent VALU chains at "
-                             "~3-4 resident waves per SIMD): neither the B_alg HBM fraction nor the "
-                             "VALU issue fraction is near 1; see DESIGN.md section 9")},
+                             "instruction issue per wave-tick at ~5 resident waves per SIMD (LDS-capped): "
+                             "neither the B_alg HBM fraction nor the VALU issue fraction is near 1; "
+                             "fewer issued instructions (register pressure, compile-time LDS offsets) "
+                             "moved the time, fewer dependent LDS round trips did not; DESIGN.md section 9")},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
