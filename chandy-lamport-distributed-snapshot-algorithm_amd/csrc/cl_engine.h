@@ -231,6 +231,9 @@ struct ExecParams {
   uint32_t* ovh;       // [C] spill ring head
   uint32_t* spilled;   // set to 1 by any push that went to a spill ring (cl_host: spill-free replays)
   int32_t nospill;     // this replay is known to fit the LDS rings: run the spill-free kernel
+  // slot -> instance for a replay (nullptr: slot i runs instance i).  cl_host orders a
+  // replay's instances by their final tick so the segments of a wave finish together
+  const int32_t* inst_map;
   // event trace of instances [trace_lo, trace_lo + trace_n) (trace kernel build only)
   TraceRec* trace;          // [trace_n][trace_cap]
   uint32_t* trace_cnt;      // [trace_n] records emitted (may exceed trace_cap: overflow)

@@ -51,6 +51,9 @@ const char* last_error() { return g_last_error.c_str(); }
 constexpr int32_t kDelayStageWords = 2048;
 // Workgroups (4 waves each) per CU the automatic FIFO sizing keeps LDS from limiting.
 constexpr int32_t kTargetBlocks = 4;
+// Batches of at least this many instances replay through a length-ordered slot map (a few
+// thousand waves: the grouping pays for its one host sort and 4 B per instance of HBM).
+constexpr int64_t kMapMinInstances = 4096;
 
 namespace {
 
@@ -268,6 +271,15 @@ struct cl_sim {
   int64_t nospill_ops = -1;
   bool spill_probe = false;    // the last launch was a fresh spill-capable full run (of probe_ops ops)
   int64_t probe_ops = 0;
+  // Replays grouped by length: after a fresh full run of ops [0, map_ops) the host orders the
+  // instances by their final tick (d_map: slot -> instance) so the 64 / N instances sharing a
+  // wave end their drains together; replays of the same program and delays launch through
+  // the map (results are per instance, unchanged).  -1: no map.
+  DevBuf<int32_t> d_map;
+  int64_t map_ops = -1;
+  bool map_probe = false;       // the last launch was a fresh unmapped full run
+  int64_t map_probe_ops = 0;
+  int64_t map_tried = -1;       // the program length a map was last built (or rejected) for
   DevBuf<int32_t> d_hist;
   DevBuf<unsigned long long> d_sums;
   // device event trace (cl_trace_enable): instances [trace_lo, trace_lo + trace_n)
@@ -288,7 +300,7 @@ struct cl_sim {
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
-      d_ovh.release(); d_spilled.release(); d_hist.release(); d_sums.release();
+      d_ovh.release(); d_spilled.release(); d_map.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       for (auto& e : ev_pool) {
         (void)hipEventDestroy(e.first);
@@ -423,6 +435,7 @@ struct cl_sim {
       HIP_TRY(hipMemcpy(d_sched.p, sched.data(), sched.size(), hipMemcpyHostToDevice));
       dev_draws = D;  // longer rows of the same streams: saved draw cursors stay valid
       nospill_ops = -1;
+      map_ops = map_tried = -1;
       dev_row = D;
       return CL_OK;
     }
@@ -438,6 +451,7 @@ struct cl_sim {
     dev_draws = user_draws;
     dev_row = row;
     nospill_ops = -1;
+    map_ops = map_tried = -1;
     return CL_OK;
   }
 
@@ -496,6 +510,7 @@ struct cl_sim {
     if ((rc = d_ovh.ensure(lay.ocap_log2 >= 0 ? (size_t)std::max(C, 1) * stride : 1))) return rc;
     if ((rc = d_spilled.ensure(1))) return rc;
     nospill_ops = -1;  // (a new layout: probe again)
+    map_ops = map_tried = -1;
     need_fresh = true;
     return CL_OK;
   }
@@ -617,6 +632,9 @@ struct cl_sim {
     // spill-free replays: a fresh full run whose program and delays already ran once without
     // touching a spill ring (the same replay fills the same queues)
     p.nospill = begin == 0 && trace_n == 0 && nospill_ops == (int64_t)ops.size() ? 1 : 0;
+    p.inst_map = begin == 0 && map_ops == (int64_t)ops.size() ? d_map.p : nullptr;
+    map_probe = begin == 0 && !p.inst_map && n_inst >= kMapMinInstances && map_tried != (int64_t)ops.size();
+    map_probe_ops = (int64_t)ops.size();
     spill_probe = begin == 0 && trace_n == 0 && !p.nospill && lay.ocap_log2 >= 0;
     if (spill_probe) {
       probe_ops = (int64_t)ops.size();
@@ -654,6 +672,44 @@ struct cl_sim {
       if (!sp) nospill_ops = probe_ops;
       spill_probe = false;
     }
+    if (map_probe) {
+      map_probe = false;
+      int rc = build_map();
+      if (rc) return rc;
+    }
+    return CL_OK;
+  }
+
+  // Slot -> instance order of the last fresh full run's final ticks (counting sort, stable).
+  int build_map() {
+    map_tried = map_probe_ops;
+    std::vector<int32_t> t((size_t)n_inst);
+    HIP_TRY(hipMemcpy(t.data(), d_regs.p + (size_t)R_TIME * stride, t.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    int32_t mx = 0;
+    for (int32_t x : t) mx = std::max(mx, std::max(x, 0));
+    std::vector<int64_t> start((size_t)mx + 2, 0);
+    for (int32_t x : t) start[(size_t)std::max(x, 0) + 1]++;
+    for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
+    std::vector<int32_t> order((size_t)n_inst);
+    for (int64_t i = 0; i < n_inst; ++i) order[(size_t)start[(size_t)std::max(t[(size_t)i], 0)]++] = (int32_t)i;
+    // worth it only when it removes wave-ticks: sum over waves of the longest instance, in
+    // launch order vs in length order (C3: 43.9 -> 39.5 ticks per wave; C2: no spread)
+    const int64_t ipw = std::max(lay.ipw, 1);
+    int64_t as_is = 0, sorted = 0;
+    for (int64_t w = 0; w < n_inst; w += ipw) {
+      int32_t a = 0, b = 0;
+      for (int64_t k = w; k < std::min<int64_t>(w + ipw, n_inst); ++k) {
+        a = std::max(a, t[(size_t)k]);
+        b = std::max(b, t[(size_t)order[(size_t)k]]);
+      }
+      as_is += a;
+      sorted += b;
+    }
+    if (sorted * 100 > as_is * 95) return CL_OK;  // under 5 % fewer wave-ticks: keep launch order
+    int rc = d_map.ensure(order.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(d_map.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    map_ops = map_probe_ops;
     return CL_OK;
   }
 
@@ -870,6 +926,7 @@ int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks) 
 int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
   SIM_CHECK(sim);
   sim->nospill_ops = -1;
+  sim->map_ops = sim->map_tried = -1;
   sim->go_seeds = true;
   sim->seed_base = seed_base;
   sim->dev_draws = -1;
@@ -880,6 +937,7 @@ int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
 int cl_set_delay_schedule(cl_sim* sim, const uint8_t* delays, int64_t draws_per_instance) {
   SIM_CHECK(sim);
   sim->nospill_ops = -1;
+  sim->map_ops = sim->map_tried = -1;
   if (!delays || draws_per_instance <= 0) return set_err(CL_E_INVALID, "empty schedule");
   const size_t n = (size_t)(draws_per_instance * sim->n_inst);
   for (size_t i = 0; i < n; ++i)

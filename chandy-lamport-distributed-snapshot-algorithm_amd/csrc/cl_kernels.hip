@@ -556,7 +556,7 @@ constexpr int waves_for(int D) {
 // pressure of the D = 3 kernel 95 VGPRs + 58 SGPR spills -> ~80 VGPRs, no spills); SPILL false
 // compiles out the HBM spill rings (a layout without them).  CAP = 0 reads every offset from
 // the runtime layout (any D, any ring size).
-template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL>
+template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
                                                                          const Op* __restrict__ ops,
                                                                          const uint8_t* __restrict__ sched) {
@@ -586,8 +586,14 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   lds_u32* X = (lds_u32*)(lds + (size_t)wib * lay.wave_words);
   const int32_t seg = lane / N;
   const int32_t v = lane - seg * N;
-  const uint32_t inst = wave * (uint32_t)lay.ipw + seg;
-  const bool valid = seg < lay.ipw && inst < p.n_inst;
+  // slot = position in the launch; inst = the instance it runs (p.inst_map: replays grouped
+  // by length so a wave's segments finish together, cl_host.cpp)
+  // (MAPPED: specialized kernels launch with a map, the others without; the generic CAP = 0
+  // kernel checks at run time)
+  const int32_t* imap = MAPPED ? p.inst_map : nullptr;
+  const uint32_t slot = wave * (uint32_t)lay.ipw + seg;
+  const bool valid = seg < lay.ipw && slot < p.n_inst;
+  const uint32_t inst = ((CAP > 0 || imap) && MAPPED && valid) ? (uint32_t)imap[slot] : slot;
   const uint32_t ii = valid ? inst : 0u;  // safe index for lanes without an instance
   const uint32_t* nb = topo + (size_t)(valid ? v : 0) * p.topo_w;
   const int32_t indeg = valid ? (int32_t)nb[0] : 0;
@@ -598,9 +604,17 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   if constexpr (STAGED) {
     const uint32_t first = wave * (uint32_t)lay.ipw;
     const uint32_t nrow = min((uint32_t)lay.ipw, (uint32_t)p.n_inst - min(first, (uint32_t)p.n_inst));
-    const uint32_t words = nrow * (uint32_t)(p.sched_row / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)first * p.sched_row);
-    for (uint32_t k = lane; k < words; k += kWave) X[lay.x_delay + k] = src[k];
+    const uint32_t rw4 = (uint32_t)(p.sched_row / 4);
+    if (!MAPPED || (CAP == 0 && !imap)) {  // consecutive instances: one contiguous copy
+      const uint32_t words = nrow * rw4;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)first * p.sched_row);
+      for (uint32_t k = lane; k < words; k += kWave) X[lay.x_delay + k] = src[k];
+    } else {  // mapped slots: row by row
+      for (uint32_t r = 0; r < nrow; ++r) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)imap[first + r] * p.sched_row);
+        for (uint32_t k = lane; k < rw4; k += kWave) X[lay.x_delay + r * rw4 + k] = src[k];
+      }
+    }
   }
   const Ctx x{p, lay, X + lay.col + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0,
@@ -859,18 +873,18 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
 
 }  // namespace
 
-template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true>
+template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true>
 int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
   const int32_t wpb = p.lay.wpb;
   const size_t lds = (size_t)p.lay.wave_words * wpb * sizeof(uint32_t);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
   const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
   const unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
-  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL>), dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)stream, p,
+  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>), dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)stream, p,
                      topo, ops, sched);
   return (int)hipGetLastError();
 }
@@ -885,15 +899,20 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
     const bool ok = p.lay.od == D && p.lay.id == D;
     if (p.lay.x_delay > 0 && ok) {
       const bool sp = p.lay.ocap_log2 >= 0 && !p.nospill;
+      const bool mp = p.inst_map != nullptr;
+#define CLSNAP_SPEC(C)                                                                              \
+  case C:                                                                                           \
+    if (sp) return mp ? launch_exec_ds<D, true, false, C, true, true>(p, topo, ops, sched, stream)   \
+                      : launch_exec_ds<D, true, false, C, true, false>(p, topo, ops, sched, stream); \
+    return mp ? launch_exec_ds<D, true, false, C, false, true>(p, topo, ops, sched, stream)          \
+              : launch_exec_ds<D, true, false, C, false, false>(p, topo, ops, sched, stream);
       switch (p.lay.cap_log2) {
-        case 1: return sp ? launch_exec_ds<D, true, false, 1, true>(p, topo, ops, sched, stream)
-                          : launch_exec_ds<D, true, false, 1, false>(p, topo, ops, sched, stream);
-        case 2: return sp ? launch_exec_ds<D, true, false, 2, true>(p, topo, ops, sched, stream)
-                          : launch_exec_ds<D, true, false, 2, false>(p, topo, ops, sched, stream);
-        case 3: return sp ? launch_exec_ds<D, true, false, 3, true>(p, topo, ops, sched, stream)
-                          : launch_exec_ds<D, true, false, 3, false>(p, topo, ops, sched, stream);
+        CLSNAP_SPEC(1)
+        CLSNAP_SPEC(2)
+        CLSNAP_SPEC(3)
         default: break;
       }
+#undef CLSNAP_SPEC
     }
   }
   return p.lay.x_delay > 0 ? launch_exec_ds<D, true, false>(p, topo, ops, sched, stream)
