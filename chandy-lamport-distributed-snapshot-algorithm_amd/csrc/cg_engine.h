@@ -140,6 +140,7 @@ struct GParams {
   uint32_t traffic_thresh;
   int64_t traffic_steps;
   int32_t n_pblocks;  // node blocks = ceil(n / kGThreads)
+  int32_t blk_max_out;  // most out-channels of any node block (k_pick's LDS stage size)
   int32_t push_lanes;  // k_push threads per node: 0 = automatic, else forced (1 or kPushLanes)
   // topology (out-CSR channel order = (src rank, dest rank); in-CSR by (dest, src))
   const int32_t* out_off;   // [n+1]

@@ -490,6 +490,9 @@ struct cl_graph {
     p.traffic_thresh = traffic_thresh;
     p.traffic_steps = traffic_steps;
     p.n_pblocks = (n + kGThreads - 1) / kGThreads;
+    p.blk_max_out = 0;
+    for (int32_t b = 0; b < p.n_pblocks; ++b)
+      p.blk_max_out = std::max(p.blk_max_out, out_off[std::min((int64_t)(b + 1) * kGThreads, (int64_t)n)] - out_off[(int64_t)b * kGThreads]);
     p.push_lanes = push_lanes;
     p.out_off = d_out_off.p;
     p.route = d_route.p;

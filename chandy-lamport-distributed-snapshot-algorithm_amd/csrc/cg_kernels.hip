@@ -309,6 +309,11 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
 // ---------------------------------------------------------------------------
 // tick phase A: pick + deliver
 // ---------------------------------------------------------------------------
+// STAGE head words staged per sender: 8 when every block has at most 8 * kGThreads
+// out-channels (16 KB of LDS: ten blocks per CU, C4), else 12 (24 KB; channels past the
+// stage are read from HBM by their sender).  C4: 9.35 -> 9.23 ms with 8; C5's hub blocks
+// are faster with 12.
+template <int STAGE>
 __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
   __shared__ int s_m;
   const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;  // drain ticks: set by k_drain_ctl
@@ -316,7 +321,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
   // contiguous CSR range, loaded once with coalesced loads (a lane-per-sender prefetch
   // touched 64 separate 64 B segments per wave instruction).  Channels past kStage
   // (blocks of unusually high out-degree) are read from HBM by their sender.
-  constexpr int kStage = kGThreads * 12;
+  constexpr int kStage = kGThreads * STAGE;
   __shared__ uint64_t s_hq[kStage];
   const int bk = p.blk_lo + (int)blockIdx.x;  // (the owned blocks in the partitioned mode)
   const int s = bk * kGThreads + threadIdx.x;
@@ -1058,6 +1063,11 @@ int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream) {
   return hipGetLastError();
 }
 
+void launch_pick(const GParams& p, dim3 grid, int32_t t, hipStream_t s) {
+  if (p.blk_max_out <= 8 * kGThreads) hipLaunchKernelGGL(k_pick<8>, grid, dim3(kGThreads), 0, s, p, t);
+  else hipLaunchKernelGGL(k_pick<12>, grid, dim3(kGThreads), 0, s, p, t);
+}
+
 // k_push lanes per node: graphs under kLanesBelow nodes (fewer than ~1 wave per SIMD at one
 // thread per node) push with kPushLanes threads per node; p.push_lanes forces either path
 // (cl_graph_set_push_lanes: the exact-match tests run both on the same graphs).
@@ -1085,7 +1095,7 @@ int cg_launch_sends(const GParams& p, int32_t t, void* stream) {
 
 int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_pick, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
+  launch_pick(p, dim3(p.n_pblocks), t, s);
   hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
   launch_push(p, t, s);
@@ -1102,7 +1112,7 @@ int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain,
   const int32_t md = max_drain > INT32_MAX ? INT32_MAX : (int32_t)max_drain;
   for (int32_t i = 0; i < ticks; ++i) {
     hipLaunchKernelGGL(k_drain_ctl, dim3(1), dim3(1), 0, s, p, n_before, md);
-    hipLaunchKernelGGL(k_pick, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, kTimeFromDevice);
+    launch_pick(p, dim3(p.n_pblocks), kTimeFromDevice, s);
     hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, kTimeFromDevice);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
     launch_push(p, kTimeFromDevice, s);
@@ -1135,7 +1145,7 @@ int cg_launch_part_pick(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
   if ((e = hipMemsetAsync(p.out_n, 0, 4 * sizeof(uint32_t), s))) return e;
-  if (p.blk_hi > p.blk_lo) hipLaunchKernelGGL(k_pick, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, t);
+  if (p.blk_hi > p.blk_lo) launch_pick(p, dim3(p.blk_hi - p.blk_lo), t, s);
   return hipGetLastError();
 }
 
