@@ -116,6 +116,11 @@ struct GScal {
   int32_t dleft;    // extra ticks left in phase 1
   int32_t dticks;   // ticks spent waiting
   int32_t dcur;     // first snapshot (< the drain's count) not yet complete
+  // drain tick i runs with slot i & 1: its time and whether it runs were decided by the
+  // previous tick's k_scan (k_drain_begin for the first), so no control kernel per tick
+  int32_t dnow;      // time of the last drain tick decided to run
+  int32_t dtime[2];
+  int32_t dskip[2];
   // parallel send group (k_sg_check -> k_sg_apply)
   int32_t sg_first;              // position of the group's first failing send (INT32_MAX: none)
   int32_t pad2;
@@ -124,7 +129,7 @@ struct GScal {
   unsigned long long tot_trig, tot_send;
 };
 enum : int32_t { kDrainWait = 0, kDrainExtra = 1, kDrainDone = 2, kDrainHang = 3 };
-constexpr int32_t kTimeFromDevice = -1;
+constexpr int32_t kTimeFromDevice = -1;  // tick argument -1 - k: drain slot k (time, skip in GScal)
 constexpr int32_t kDrainExtraTicks = 6;  // maxDelay + 1 (test_common.go:135-137)  // tick argument: read the tick's time from GScal.time
 
 struct GParams {
@@ -201,8 +206,9 @@ int cg_launch_tick(const GParams& p, int32_t t, void* stream);
 // [0, n_before), then `ticks` x (k_drain_ctl + one tick whose time comes from GScal):
 // k_drain_ctl decides on the device whether the tick runs (waiting, then maxDelay+1 extra
 // ticks) or is skipped (drain over / hung), so the host checks only once per batch.
-int cg_launch_drain_begin(const GParams& p, void* stream);
-int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain, int32_t ticks, void* stream);
+int cg_launch_drain_begin(const GParams& p, int32_t time, int32_t n_before, int64_t max_drain, void* stream);
+int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain, int64_t first, int32_t ticks,
+                          void* stream);
 int cg_launch_drain_end(const GParams& p, void* stream);  // normal ticks run again
 int cg_launch_sends(const GParams& p, int32_t t, void* stream);  // step-0 traffic
 int cg_launch_hostops(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream);

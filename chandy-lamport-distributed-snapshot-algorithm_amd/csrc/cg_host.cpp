@@ -606,13 +606,15 @@ struct cl_graph {
   // loop runs on the device (k_drain_ctl before every tick decides whether it runs), so
   // the host launches ticks in growing batches and reads the drain state once per batch.
   int run_drain(int32_t n_before) {
-    int rc = k_err(cg_launch_drain_begin(P, stream));
+    int rc = k_err(cg_launch_drain_begin(P, (int32_t)time, n_before, max_drain, stream));
     if (rc) return rc;
     const int32_t time0 = (int32_t)time;
     int32_t batch = 8;
+    int64_t launched = 0;  // drain ticks launched (tick i uses control slot i & 1)
     GScal sc;
     for (;;) {
-      if ((rc = k_err(cg_launch_drain_ticks(P, n_before, max_drain, batch, stream)))) return rc;
+      if ((rc = k_err(cg_launch_drain_ticks(P, n_before, max_drain, launched, batch, stream)))) return rc;
+      launched += batch;
       GHIP(hipMemcpyAsync(&sc, d_sc.p, sizeof sc, hipMemcpyDeviceToHost, stream));
       GHIP(hipStreamSynchronize(stream));
       if (sc.status || sc.dphase == kDrainDone || sc.dphase == kDrainHang) break;

@@ -73,11 +73,16 @@ __device__ inline void block_count(const GParams& p, const int (&idx)[NV], unsig
 
 // Frozen-run check, uniform over the block (a status set by another block of the same
 // kernel must not split a block at a barrier).
-__device__ inline bool block_frozen(const GParams& p) {
+__device__ inline bool block_frozen(const GParams& p, int32_t targ = 0) {
   __shared__ int s_frozen;
-  if (threadIdx.x == 0) s_frozen = p.sc->status | p.sc->skip;
+  if (threadIdx.x == 0) s_frozen = p.sc->status | (targ >= 0 ? p.sc->skip : p.sc->dskip[-1 - targ]);
   __syncthreads();
   return s_frozen != 0;
+}
+
+// A tick's time: the argument, or its drain slot's (targ = -1 - slot).
+__device__ inline int32_t tick_time(const GParams& p, int32_t targ) {
+  return targ >= 0 ? targ : p.sc->dtime[-1 - targ];
 }
 
 __device__ inline void set_status(GScal* sc, int32_t code) { atomicCAS(&sc->status, 0, code); }
@@ -235,25 +240,17 @@ __device__ inline int expand_range(const GParams& p, int32_t t, int32_t s0, int3
 // ---------------------------------------------------------------------------
 // device-side drain (test_common.go:123-137)
 // ---------------------------------------------------------------------------
-__global__ void k_drain_begin(GParams p) {
-  GScal* sc = p.sc;
-  sc->dphase = kDrainWait;
-  sc->dleft = 0;
-  sc->dticks = 0;
-  sc->dcur = 0;
-  sc->skip = 0;
-}
-
-// Before each drain tick (one thread): the reference's loop `select { case <-getSnapshots:
-// ...; default: sim.Tick() }` until every snapshot started before the drain was collected,
-// then maxDelay+1 more ticks.  Completion is checked before the tick, as the host loop did;
-// snapshot completions are permanent, so a cursor over [0, n_before) makes the check O(1)
-// amortized.  A run that needs more than max_drain waiting ticks hangs (status HANG on the
-// host) -- the reference would loop forever.
-__global__ void k_drain_ctl(GParams p, int32_t n_before, int32_t max_drain) {
+// The reference's loop `select { case <-getSnapshots: ...; default: sim.Tick() }` until every
+// snapshot started before the drain was collected, then maxDelay+1 more ticks: decided for
+// the NEXT drain tick into `slot` (one thread).  Completion is checked before the tick, as
+// the host loop did -- completions happen in k_marker, before k_scan decides; snapshot
+// completions are permanent, so a cursor over [0, n_before) makes the check O(1) amortized.
+// A run that needs more than max_drain waiting ticks hangs (status HANG on the host) -- the
+// reference would loop forever.
+__device__ inline void drain_decide(const GParams& p, int32_t n_before, int32_t max_drain, int32_t slot) {
   GScal* sc = p.sc;
   if (sc->status) {
-    sc->skip = 1;
+    sc->dskip[slot] = 1;
     return;
   }
   int32_t ph = sc->dphase;
@@ -266,25 +263,36 @@ __global__ void k_drain_ctl(GParams p, int32_t n_before, int32_t max_drain) {
       sc->dleft = kDrainExtraTicks;
     } else if (sc->dticks >= max_drain) {
       sc->dphase = kDrainHang;
-      sc->skip = 1;
+      sc->dskip[slot] = 1;
       return;
     } else {
       sc->dticks += 1;
-      sc->time += 1;  // time++ of the tick that follows (sim.go:72)
-      sc->skip = 0;
+      sc->dtime[slot] = ++sc->dnow;  // time++ of the tick that follows (sim.go:72)
+      sc->dskip[slot] = 0;
       return;
     }
   }
   if (ph == kDrainExtra && sc->dleft > 0) {
     sc->dleft -= 1;
     sc->dphase = ph;
-    sc->time += 1;
-    sc->skip = 0;
+    sc->dtime[slot] = ++sc->dnow;
+    sc->dskip[slot] = 0;
     return;
   }
   if (ph == kDrainExtra) ph = kDrainDone;
   sc->dphase = ph;
-  sc->skip = 1;
+  sc->dskip[slot] = 1;
+}
+
+__global__ void k_drain_begin(GParams p, int32_t time, int32_t n_before, int32_t max_drain) {
+  GScal* sc = p.sc;
+  sc->dphase = kDrainWait;
+  sc->dleft = 0;
+  sc->dticks = 0;
+  sc->dcur = 0;
+  sc->skip = 0;
+  sc->dnow = time;
+  drain_decide(p, n_before, max_drain, 0);  // the first drain tick
 }
 
 __global__ void k_drain_end(GParams p) { p.sc->skip = 0; }
@@ -316,7 +324,7 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
 template <int STAGE>
 __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
   __shared__ int s_m;
-  const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;  // drain ticks: set by k_drain_ctl
+  const int32_t t = tick_time(p, targ);  // (drain ticks: decided by the previous tick's k_scan)
   // Head receiveTime words of the block's senders: the block's out-channels are one
   // contiguous CSR range, loaded once with coalesced loads (a lane-per-sender prefetch
   // touched 64 separate 64 B segments per wave instruction).  Channels past kStage
@@ -334,7 +342,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
     od = p.out_off[s + 1] - base;
   }
   // (topology loads above are in flight during the status check: one latency, not two)
-  if (block_frozen(p)) return;
+  if (block_frozen(p, targ)) return;
   if (threadIdx.x == 0) s_m = 0;
   {
     // all loads issued before the first LDS store: one HBM latency, not one per stride
@@ -416,7 +424,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
 // (k_tally), so k_marker only records the triggers.
 template <bool REMOTE>
 __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
-  const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;
+  const int32_t t = tick_time(p, targ);
   const int bk = REMOTE ? (int)blockIdx.x : p.blk_lo + (int)blockIdx.x;
   const MDel* list = REMOTE ? p.rmlist + (size_t)bk * kGThreads : p.mlist + (size_t)bk * kGThreads;
   // the tally's inputs (node tokens after this tick's deliveries, out-degree) and the
@@ -424,7 +432,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   const int32_t sendbit = p.part ? 0 : tally_send_bit(p, bk, t);
   const int nm = REMOTE ? min(kGThreads, (int)p.out_n[1] - bk * kGThreads) : p.mcnt[bk];
   if (REMOTE && nm <= 0) return;
-  if (block_frozen(p)) return;
+  if (block_frozen(p, targ)) return;
   __shared__ int s_nb, s_base;
   __shared__ int s_trig[kGThreads];
   // local snapshots created by this block's markers at nodes of in-degree <= kSmallIndeg,
@@ -540,8 +548,11 @@ __global__ void __launch_bounds__(kGThreads) k_tally(GParams p, int32_t step) {
 
 // phase C: exclusive scan of the block tallies (one workgroup, 4 entries per thread),
 // draw bases
-__global__ void __launch_bounds__(1024) k_scan(GParams p) {
-  if (block_frozen(p)) return;
+__global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t n_before, int32_t max_drain) {
+  if (block_frozen(p, targ)) {
+    if (targ < 0 && threadIdx.x == 0) drain_decide(p, n_before, max_drain, (-1 - targ) ^ 1);  // (stays frozen)
+    return;
+  }
   __shared__ long long sh[32];
   long long carry_a = 0, carry_b = 0;
   for (int c0 = p.blk_lo; c0 < p.blk_hi; c0 += 4 * blockDim.x) {
@@ -578,6 +589,7 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p) {
     p.sc->base_send = d + (unsigned long long)carry_a;
     p.sc->draw = d + (unsigned long long)(carry_a + carry_b);
   }
+  if (targ < 0 && threadIdx.x == 0) drain_decide(p, n_before, max_drain, (-1 - targ) ^ 1);  // the next drain tick
 }
 
 // The r-th local snapshot created at v this tick in creating-sender order (prev = the
@@ -715,8 +727,8 @@ __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, i
 // then the grid expands the local snapshots created at high in-degree nodes.
 template <int L>
 __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int32_t sarg) {
-  const int32_t t = targ != kTimeFromDevice ? targ : p.sc->time;
-  const int32_t step = sarg != kTimeFromDevice ? sarg : t;  // the traffic of step t follows tick t
+  const int32_t t = tick_time(p, targ);
+  const int32_t step = sarg >= 0 ? sarg : t;  // the traffic of step t follows tick t
   const int64_t gid = ((int64_t)p.blk_lo * kGThreads * L) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int v = (int)(gid / L), jl = (int)(gid % L);
   int32_t ob = 0, od = 0, ncre = 0, tok = 0;
@@ -726,7 +738,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
     ncre = p.crn[v];
     tok = p.tokens[v];
   }
-  if (block_frozen(p)) return;
+  if (block_frozen(p, targ)) return;
   unsigned long long c[2] = {0, 0};  // push, peek
   if (v < p.part_hi) {
     int32_t tj = -1;
@@ -1088,7 +1100,7 @@ void launch_push(const GParams& p, int32_t t, hipStream_t s) { launch_push(p, t,
 int cg_launch_sends(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_tally, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p, 0, 0, 0);
   launch_push(p, t, s);
   return hipGetLastError();
 }
@@ -1097,25 +1109,29 @@ int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   launch_pick(p, dim3(p.n_pblocks), t, s);
   hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p, t, 0, 0);
   launch_push(p, t, s);
   return hipGetLastError();
 }
 
-int cg_launch_drain_begin(const GParams& p, void* stream) {
-  hipLaunchKernelGGL(k_drain_begin, dim3(1), dim3(1), 0, (hipStream_t)stream, p);
+int cg_launch_drain_begin(const GParams& p, int32_t time, int32_t n_before, int64_t max_drain, void* stream) {
+  const int32_t md = max_drain > INT32_MAX ? INT32_MAX : (int32_t)max_drain;
+  hipLaunchKernelGGL(k_drain_begin, dim3(1), dim3(1), 0, (hipStream_t)stream, p, time, n_before, md);
   return hipGetLastError();
 }
 
-int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain, int32_t ticks, void* stream) {
+// Drain ticks first .. first + ticks - 1 of this drain: tick i reads its time and whether it
+// runs from slot i & 1, and its k_scan decides tick i + 1 into the other slot.
+int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain, int64_t first, int32_t ticks,
+                          void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int32_t md = max_drain > INT32_MAX ? INT32_MAX : (int32_t)max_drain;
   for (int32_t i = 0; i < ticks; ++i) {
-    hipLaunchKernelGGL(k_drain_ctl, dim3(1), dim3(1), 0, s, p, n_before, md);
-    launch_pick(p, dim3(p.n_pblocks), kTimeFromDevice, s);
-    hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, kTimeFromDevice);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
-    launch_push(p, kTimeFromDevice, s);
+    const int32_t ta = -1 - (int32_t)((first + i) & 1);
+    launch_pick(p, dim3(p.n_pblocks), ta, s);
+    hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, ta);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p, ta, n_before, md);
+    launch_push(p, ta, ta, s);
   }
   return hipGetLastError();
 }
@@ -1163,7 +1179,7 @@ int cg_launch_part_tally(const GParams& p, int32_t step, const int2* rep, int32_
   hipStream_t s = (hipStream_t)stream;
   if (n_rep > 0) hipLaunchKernelGGL(k_part_trig, dim3((n_rep + kGThreads - 1) / kGThreads), dim3(kGThreads), 0, s, p, rep, n_rep);
   if (p.blk_hi > p.blk_lo) hipLaunchKernelGGL(k_tally, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, step);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p, 0, 0, 0);
   return hipGetLastError();
 }
 
