@@ -83,6 +83,7 @@ def lib():
         "cl_last_kernel_ms": [vp, vp],
         "cl_kernel_time": [vp, vp, vp],
         "cl_replay_spill_free": [vp, vp],
+        "cl_replay_mapped": [vp, vp],
         "cl_num_nodes": [vp, vp],
         "cl_node_id": [vp, i32, vp],
         "cl_num_channels": [vp, vp],
@@ -371,6 +372,12 @@ class ChandyLamportSim:
         """True when the next rerun() runs the spill-free kernel (cl_replay_spill_free)."""
         v = C.c_int32(0)
         _check(self._L.cl_replay_spill_free(self._h, C.byref(v)))
+        return bool(v.value)
+
+    def mapped_replays(self):
+        """True when the next rerun() launches through the length-ordered slot map."""
+        v = C.c_int32(0)
+        _check(self._L.cl_replay_mapped(self._h, C.byref(v)))
         return bool(v.value)
 
     def kernel_time(self):

@@ -1073,6 +1073,15 @@ int cl_replay_spill_free(cl_sim* sim, int32_t* on) {
   return CL_OK;
 }
 
+int cl_replay_mapped(cl_sim* sim, int32_t* on) {
+  SIM_CHECK(sim);
+  if (!on) return set_err(CL_E_INVALID, "null output");
+  int rc = sim->sync();  // (a pending map probe is evaluated here)
+  if (rc) return rc;
+  *on = sim->map_ops == (int64_t)sim->ops.size() ? 1 : 0;
+  return CL_OK;
+}
+
 int cl_synchronize(cl_sim* sim) {
   SIM_CHECK(sim);
   return sim->sync();

@@ -146,6 +146,10 @@ int cl_kernel_time(cl_sim* sim, double* total_ms, int64_t* launches);
  * so its replays fill the same LDS queues (engine-internal specialization; results are the
  * same either way). */
 int cl_replay_spill_free(cl_sim* sim, int32_t* on);
+/* 1 in *on when the next cl_rerun launches through the length-ordered slot map (instances
+ * grouped by the final tick of an earlier full run of the same program and delays, so the
+ * instances sharing a wave finish together; engine-internal, results unchanged). */
+int cl_replay_mapped(cl_sim* sim, int32_t* on);
 
 /* ---- topology queries (host only) ---------------------------------------- */
 int cl_num_nodes(const cl_sim* sim, int32_t* n);

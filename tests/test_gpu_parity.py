@@ -251,6 +251,10 @@ def test_rerun_equals_flush_and_oracle(cfg):
     first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
     if slots == 2:  # two LDS slots: deep channels must have used the HBM spill rings
         assert not sim.spill_free_replays()
+    if n == 131072 and slots is None:  # C3: instance lengths spread (13..50 ticks): mapped replays
+        assert sim.mapped_replays()
+    if n == 65536:  # C2: too little spread to pay for the map
+        assert not sim.mapped_replays()
     _, st, ticks, cnt, hashes = oracle_batch(top, events, n, threads=16)
     want = batch_sums_from_oracle(st, cnt, hashes)
     for r in range(3):
