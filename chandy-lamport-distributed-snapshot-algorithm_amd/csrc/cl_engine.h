@@ -87,7 +87,7 @@ struct TraceRec {
 //   bit 31 marker, bit 30 valid, bits 22..16 out-index, bits 15..0 payload.
 constexpr uint32_t kPickValid = 0x40000000u;
 
-// Per-instance results written at the end of every launch (regs[r * stride + inst]).
+// Per-instance results written at the end of every launch (regs[inst * R_NUM + r]).
 enum : int32_t {
   R_TIME = 0,
   R_DRAW = 1,
@@ -217,16 +217,16 @@ struct ExecParams {
   int64_t n_inst, stride;
   int32_t fresh;       // start from the initial topology state (else resume from `state`)
   int32_t save_state;  // write the resumable state image at the end
-  // state: [state_words][stride]; regs: [R_NUM][stride]
+  // state: [state_words][stride]; regs: [stride][R_NUM]
   uint32_t* state;
-  int32_t* regs;
+  int32_t* regs;       // [stride][R_NUM] per-instance results
   // outputs, node index fastest so a wave's stores coalesce:
   int32_t* fin_tok;    // [stride][N]          final node tokens
   // [S_cap][stride][N][rw] one record per (snapshot, node), written when the node creates its
   // local snapshot: word 0 = tokenMap entry, word 1 + k = recording cursors of in-link k
   // (lo16 = begin, hi16 = end, the end written when the channel's marker arrives)
   uint32_t* snap_nod;
-  int32_t* snap_tick;  // [S_cap][stride]      completion tick or -1
+  int32_t* snap_tick;  // [stride][S_cap]      completion tick or -1 (one row per instance)
   uint32_t* ovf;       // [C][1 << ocap_log2] spill ring
   uint32_t* ovh;       // [C] spill ring head
   uint32_t* spilled;   // set to 1 by any push that went to a spill ring (cl_host: spill-free replays)

@@ -684,7 +684,8 @@ struct cl_sim {
   int build_map() {
     map_tried = map_probe_ops;
     std::vector<int32_t> t((size_t)n_inst);
-    HIP_TRY(hipMemcpy(t.data(), d_regs.p + (size_t)R_TIME * stride, t.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy2D(t.data(), sizeof(int32_t), d_regs.p + R_TIME, R_NUM * sizeof(int32_t), sizeof(int32_t), t.size(),
+                        hipMemcpyDeviceToHost));
     int32_t mx = 0;
     for (int32_t x : t) mx = std::max(mx, std::max(x, 0));
     // one global counting sort by final tick (sorting within windows of 64 waves instead, to
@@ -738,23 +739,19 @@ struct cl_sim {
   int count_complete(int32_t sid, int64_t lo, int64_t hi, int64_t* n, int64_t* n_frozen = nullptr) {
     int rc = flush();
     if (rc) return rc;
-    const int32_t *t, *st;
-    std::vector<int32_t> plane, stat;
+    std::vector<int32_t> plane((size_t)std::max<int64_t>(hi - lo, 0)), stat(plane.size());
     if (h_valid) {
-      t = h_snap_tick.data() + (size_t)sid * stride + lo;
-      st = h_regs.data() + (size_t)R_STATUS * stride + lo;
-    } else {
-      plane.resize((size_t)(hi - lo));
-      stat.resize((size_t)(hi - lo));
-      if (hi > lo) {
-        HIP_TRY(hipMemcpy(plane.data(), d_snap_tick.p + (size_t)sid * stride + lo, plane.size() * sizeof(int32_t),
-                          hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(stat.data(), d_regs.p + (size_t)R_STATUS * stride + lo, stat.size() * sizeof(int32_t),
-                          hipMemcpyDeviceToHost));
+      for (int64_t i = lo; i < hi; ++i) {
+        plane[(size_t)(i - lo)] = tick_at(sid, i);
+        stat[(size_t)(i - lo)] = reg(i, R_STATUS);
       }
-      t = plane.data();
-      st = stat.data();
+    } else if (hi > lo) {  // (instance-major rows: one strided copy each)
+      HIP_TRY(hipMemcpy2D(plane.data(), sizeof(int32_t), d_snap_tick.p + (size_t)lo * s_cap + sid, s_cap * sizeof(int32_t),
+                          sizeof(int32_t), plane.size(), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy2D(stat.data(), sizeof(int32_t), d_regs.p + (size_t)lo * R_NUM + R_STATUS, R_NUM * sizeof(int32_t),
+                          sizeof(int32_t), stat.size(), hipMemcpyDeviceToHost));
     }
+    const int32_t *t = plane.data(), *st = stat.data();
     int64_t c = 0, f = 0;
     for (int64_t i = 0; i < hi - lo; ++i) {
       c += t[i] >= 0;
@@ -788,6 +785,8 @@ struct cl_sim {
   const uint32_t* rec_base(int sid, int64_t inst) const {
     return &h_snap_nod[((size_t)sid * stride + inst) * ids.size() * lay.rw];
   }
+  int32_t reg(int64_t inst, int r) const { return h_regs[(size_t)inst * R_NUM + r]; }
+  int32_t tick_at(int sid, int64_t inst) const { return h_snap_tick[(size_t)inst * s_cap + sid]; }
   int32_t tok_at(int sid, int64_t inst, int v) const { return (int32_t)rec_base(sid, inst)[(size_t)v * lay.rw]; }
   uint32_t rec_at(int sid, int64_t inst, int c) const { return rec_base(sid, inst)[ch_slot[c]]; }
 
@@ -1179,7 +1178,7 @@ int cl_get_status(cl_sim* sim, int32_t* out) {
   SIM_CHECK(sim);
   int rc = sim->fetch();
   if (rc) return rc;
-  std::memcpy(out, sim->h_regs.data() + (size_t)R_STATUS * sim->stride, sim->n_inst * 4);
+  for (int64_t i = 0; i < sim->n_inst; ++i) out[i] = sim->reg(i, R_STATUS);
   return CL_OK;
 }
 
@@ -1187,7 +1186,7 @@ int cl_get_time(cl_sim* sim, int32_t* out) {
   SIM_CHECK(sim);
   int rc = sim->fetch();
   if (rc) return rc;
-  std::memcpy(out, sim->h_regs.data() + (size_t)R_TIME * sim->stride, sim->n_inst * 4);
+  for (int64_t i = 0; i < sim->n_inst; ++i) out[i] = sim->reg(i, R_TIME);
   return CL_OK;
 }
 
@@ -1207,7 +1206,7 @@ int cl_snapshot_tick(cl_sim* sim, int32_t sid, int64_t inst, int32_t* tick) {
     return set_err(CL_E_INVALID, "snapshot/instance out of range");
   int rc = sim->fetch();
   if (rc) return rc;
-  *tick = sim->h_snap_tick[(size_t)sid * sim->stride + inst];
+  *tick = sim->tick_at(sid, inst);
   return CL_OK;
 }
 
@@ -1218,8 +1217,7 @@ int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens,
     return set_err(CL_E_INVALID, "snapshot/instance out of range");
   int rc = sim->fetch();
   if (rc) return rc;
-  const size_t st = sim->stride;
-  if (sim->h_snap_tick[(size_t)sid * st + inst] < 0)
+  if (sim->tick_at(sid, inst) < 0)
     return set_err(CL_E_NOT_COMPLETE, "snapshot %d has not completed in instance %lld", sid, (long long)inst);
   const int n = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
   for (int v = 0; v < n; ++v) tokens[v] = sim->tok_at(sid, inst, v);
@@ -1280,13 +1278,12 @@ int cl_collect_snapshot_range(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t
     return set_err(CL_E_INVALID, "snapshot/instance range out of range");
   int rc = sim->fetch();
   if (rc) return rc;
-  const size_t st = sim->stride;
   const int n = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
   int64_t m = 0;
   bool fits = true;
   for (int64_t i = inst_lo; i < inst_hi; ++i) {
     const int64_t r = i - inst_lo;
-    const bool done = sim->h_snap_tick[(size_t)sid * st + i] >= 0;
+    const bool done = sim->tick_at(sid, i) >= 0;
     if (complete) complete[r] = done ? 1 : 0;
     if (tokens)
       for (int v = 0; v < n; ++v) tokens[r * n + v] = done ? sim->tok_at(sid, i, v) : -1;
@@ -1310,20 +1307,19 @@ int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out) {
   int rc = sim->fetch();
   if (rc) return rc;
   for (int k = 0; k < CL_NUM_COUNTERS; ++k) out[k] = 0;
-  const size_t st = sim->stride;
   const int C = (int)sim->ch_dst.size();
-  const int32_t* R = sim->h_regs.data();
+
   for (int64_t i = 0; i < sim->n_inst; ++i) {
-    if (only_ok && R[R_STATUS * st + i] != ST_OK) continue;
-    out[CL_CNT_PUSH] += (uint32_t)R[R_PUSH * st + i];
-    out[CL_CNT_PEEK] += (uint32_t)R[R_PEEK * st + i];
-    out[CL_CNT_POP_TOKEN] += (uint32_t)R[R_POP_TOK * st + i];
-    out[CL_CNT_POP_MARKER] += (uint32_t)R[R_POP_MK * st + i];
-    out[CL_CNT_COMPLETED] += R[R_NDONE * st + i];
+    if (only_ok && sim->reg(i, R_STATUS) != ST_OK) continue;
+    out[CL_CNT_PUSH] += (uint32_t)sim->reg(i, R_PUSH);
+    out[CL_CNT_PEEK] += (uint32_t)sim->reg(i, R_PEEK);
+    out[CL_CNT_POP_TOKEN] += (uint32_t)sim->reg(i, R_POP_TOK);
+    out[CL_CNT_POP_MARKER] += (uint32_t)sim->reg(i, R_POP_MK);
+    out[CL_CNT_COMPLETED] += sim->reg(i, R_NDONE);
     out[CL_CNT_INSTANCES] += 1;
-    out[CL_CNT_TICKS] += R[R_TIME * st + i];
+    out[CL_CNT_TICKS] += sim->reg(i, R_TIME);
     for (int32_t s = 0; s < sim->n_sids; ++s) {
-      if (sim->h_snap_tick[(size_t)s * st + i] < 0) continue;
+      if (sim->tick_at(s, i) < 0) continue;
       for (int c = 0; c < C; ++c) {
         const uint32_t rec = sim->rec_at(s, i, c);
         out[CL_CNT_RECORDED] += (rec >> 16) - (rec & 0xffffu);

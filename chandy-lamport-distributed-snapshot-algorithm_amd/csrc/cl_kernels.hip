@@ -67,7 +67,7 @@ struct Ctx {
   int32_t indeg, outdeg, out_off;
   // snapshot outputs by 32-bit byte offsets from the (uniform) array bases: the stores use
   // the SGPR-base + 32-bit-VGPR-offset form, with no 64-bit address arithmetic per store
-  uint32_t nod_plane, tick_plane;  // bytes per sid plane (uniform)
+  uint32_t nod_plane;  // bytes per sid plane of the node records (uniform)
   bool mul24;  // every plane offset sid * plane fits the 24-bit multiplier
 };
 
@@ -202,7 +202,12 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
     if (lay.ocap_log2 < 0 || cnt - cap >= (1u << lay.ocap_log2)) { ln.flag = ST_FIFO_OVERFLOW; return; }
     const uint32_t c = (uint32_t)(x.out_off + ko);
     const uint32_t om = (1u << lay.ocap_log2) - 1;
-    const uint32_t h = x.p.ovh[c * x.stride + x.inst];
+    uint32_t* hp = &x.p.ovh[c * x.stride + x.inst];
+    // nothing spilled yet (cnt == cap): the ring restarts at slot 0, so its head needs no
+    // reset per run -- spill rings are touched only by pushes that spill
+    uint32_t h = 0;
+    if (cnt == cap) *hp = 0u;
+    else h = *hp;
     x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.stride + x.inst] = e;
     *x.p.spilled = 1u;  // (a replay of this program needs the spill rings)
   }
@@ -251,7 +256,7 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
 __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
   const uint32_t old = lds_add(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
   if (old + 1 == (uint32_t)x.p.n_nodes) {
-    st_snap(x.p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + 4u * x.inst, ln.time);
+    st_snap(x.p.snap_tick, 4u * (x.inst * (uint32_t)x.lay.s_cap + (uint32_t)sid), ln.time);
     lds_add(&XW(x.lay.x_ndone + x.seg), 1u);
   }
 }
@@ -618,7 +623,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   }
   const Ctx x{p, lay, X + lay.col + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0,
-              4u * st * (uint32_t)N * (uint32_t)lay.rw, 4u * st,
+              4u * st * (uint32_t)N * (uint32_t)lay.rw,
               4ull * st * (uint64_t)N * (uint64_t)lay.rw < (1ull << 24)};
   InLinks<D> it;
   if constexpr (unrolled(D)) {
@@ -640,11 +645,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     // orders these stores before any completion store of the same wave
     if (valid)
       for (int32_t sid = v; sid < lay.s_cap; sid += N)
-        st_at(p.snap_tick, plane_off(x, (uint32_t)sid, x.tick_plane) + 4u * x.inst, (int32_t)-1);
-    // HBM spill ring heads start at 0 likewise: every lane owns its out-channels' heads
-    // (only their sender pushes, refills and counts them)
-    if (valid && lay.ocap_log2 >= 0)
-      for (int32_t ko = 0; ko < outdeg; ++ko) p.ovh[(uint32_t)(x.out_off + ko) * st + ii] = 0u;
+        st_at(p.snap_tick, 4u * (x.inst * (uint32_t)lay.s_cap + (uint32_t)sid), (int32_t)-1);
     __builtin_amdgcn_s_waitcnt(0);
     for (int32_t k = 0; k < lay.priv; ++k) PW(k) = 0u;
     ln.tokens = valid ? (int32_t)topo[(size_t)N * p.topo_w + v] : 0;
@@ -780,16 +781,16 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   p.fin_tok[ii * (uint32_t)N + v] = ln.tokens;
   if (v == 0) {
     const lds_u32* acc = &XW(lay.x_acc + 5 * seg);
-    int32_t* r = p.regs + ii;
-    r[R_TIME * st] = ln.time;
-    r[R_DRAW * st] = ln.draw;
-    r[R_STATUS * st] = ln.status;
-    r[R_NDONE * st] = (int32_t)XW(lay.x_ndone + seg);
-    r[R_PEEK * st] = (int32_t)acc[0];
-    r[R_POP_TOK * st] = (int32_t)acc[1];
-    r[R_POP_MK * st] = (int32_t)acc[2];
-    r[R_PUSH * st] = (int32_t)acc[3];
-    r[R_INFLIGHT_TOK * st] = (int32_t)acc[4];
+    int32_t* r = p.regs + (size_t)ii * R_NUM;  // one 36-byte row per instance
+    r[R_TIME] = ln.time;
+    r[R_DRAW] = ln.draw;
+    r[R_STATUS] = ln.status;
+    r[R_NDONE] = (int32_t)XW(lay.x_ndone + seg);
+    r[R_PEEK] = (int32_t)acc[0];
+    r[R_POP_TOK] = (int32_t)acc[1];
+    r[R_POP_MK] = (int32_t)acc[2];
+    r[R_PUSH] = (int32_t)acc[3];
+    r[R_INFLIGHT_TOK] = (int32_t)acc[4];
   }
   if (!p.save_state) return;
   uint32_t* S = p.state + ii;
@@ -820,20 +821,20 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
 __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
   const int64_t inst = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (inst >= p.n_inst) return;
-  const int32_t* r = p.regs + inst;
-  const int32_t st = r[R_STATUS * p.stride];
+  const int32_t* r = p.regs + inst * R_NUM;
+  const int32_t st = r[R_STATUS];
   unsigned long long v[10] = {1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (st == ST_OK) v[1] = 1;
   else if (st == ST_FATAL_INSUFFICIENT || st == ST_FATAL_UNKNOWN_DEST) v[2] = 1;
   else v[3] = 1;
   if (st == ST_OK) {
-    v[4] = (unsigned long long)(uint32_t)r[R_POP_TOK * p.stride] + (uint32_t)r[R_POP_MK * p.stride];
-    const int32_t inflight = r[R_INFLIGHT_TOK * p.stride];
+    v[4] = (unsigned long long)(uint32_t)r[R_POP_TOK] + (uint32_t)r[R_POP_MK];
+    const int32_t inflight = r[R_INFLIGHT_TOK];
     v[9] = (unsigned long long)inflight;
     uint64_t hsum = 0, cut = 0;
     int64_t ncomplete = 0;
     for (int32_t sid = 0; sid < p.n_sids; ++sid) {
-      if (p.snap_tick[(int64_t)sid * p.stride + inst] < 0) continue;
+      if (p.snap_tick[inst * p.s_cap + sid] < 0) continue;
       ncomplete++;
       uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)sid;
       int64_t total = 0;
