@@ -341,18 +341,18 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
     base = p.out_off[s];
     od = p.out_off[s + 1] - base;
   }
-  // (topology loads above are in flight during the status check: one latency, not two)
+  // all stage loads issued before the first LDS store (one HBM latency, not one per
+  // stride), and before the status check: topology, head words and the check overlap
+  constexpr int kPer = kStage / kGThreads;
+  uint64_t tmp[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int32_t i = threadIdx.x + k * kGThreads;
+    tmp[k] = i < nst ? p.hq[blo + i] : 0;
+  }
   if (block_frozen(p, targ)) return;
   if (threadIdx.x == 0) s_m = 0;
   {
-    // all loads issued before the first LDS store: one HBM latency, not one per stride
-    constexpr int kPer = kStage / kGThreads;
-    uint64_t tmp[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int32_t i = threadIdx.x + k * kGThreads;
-      tmp[k] = i < nst ? p.hq[blo + i] : 0;
-    }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int32_t i = threadIdx.x + k * kGThreads;
@@ -549,6 +549,18 @@ __global__ void __launch_bounds__(kGThreads) k_tally(GParams p, int32_t step) {
 // phase C: exclusive scan of the block tallies (one workgroup, 4 entries per thread),
 // draw bases
 __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t n_before, int32_t max_drain) {
+  // the first chunk of block tallies is loaded while the status check is in flight (one
+  // latency, not two: this single-workgroup kernel is pure latency, ~6 us per tick)
+  long long pa[4], pb[4];
+  {
+    const int i0 = p.blk_lo + 4 * threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool in = i0 + q < p.blk_hi;
+      pa[q] = in ? p.bsum[2 * (i0 + q)] : 0;
+      pb[q] = in ? p.bsum[2 * (i0 + q) + 1] : 0;
+    }
+  }
   if (block_frozen(p, targ)) {
     if (targ < 0 && threadIdx.x == 0) drain_decide(p, n_before, max_drain, (-1 - targ) ^ 1);  // (stays frozen)
     return;
@@ -560,8 +572,8 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t 
     long long va[4], vb[4], a = 0, b = 0;
     for (int q = 0; q < 4; ++q) {
       const bool in = i0 + q < p.blk_hi;
-      va[q] = in ? p.bsum[2 * (i0 + q)] : 0;
-      vb[q] = in ? p.bsum[2 * (i0 + q) + 1] : 0;
+      va[q] = c0 == p.blk_lo ? pa[q] : in ? p.bsum[2 * (i0 + q)] : 0;
+      vb[q] = c0 == p.blk_lo ? pb[q] : in ? p.bsum[2 * (i0 + q) + 1] : 0;
       a += va[q];
       b += vb[q];
     }
