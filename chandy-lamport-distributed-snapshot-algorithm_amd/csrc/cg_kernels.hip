@@ -431,6 +431,9 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   // block's marker count are loaded while the status check is in flight
   const int32_t sendbit = p.part ? 0 : tally_send_bit(p, bk, t);
   const int nm = REMOTE ? min(kGThreads, (int)p.out_n[1] - bk * kGThreads) : p.mcnt[bk];
+  // (the block's marker row too -- its kGThreads slots are allocated whatever nm is)
+  MDel mpre{};
+  if (!REMOTE) mpre = list[threadIdx.x];
   if (REMOTE && nm <= 0) return;
   if (block_frozen(p, targ)) return;
   __shared__ int s_nb, s_base;
@@ -456,7 +459,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   int bslot = -1, cslot = -1;
   BigX bx;
   if ((int)threadIdx.x < nm) {
-    const MDel m = list[threadIdx.x];
+    const MDel m = REMOTE ? list[threadIdx.x] : mpre;
     const int32_t s0 = m.s0, v = m.v, k = m.k;
     sid = m.sid;
     vdone = v;
@@ -648,14 +651,15 @@ __device__ inline void push_q(const GParams& p, int32_t c, uint64_t& q, uint32_t
 constexpr int kRegOd = 8;
 template <int R>
 __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int32_t ob, int32_t od, int ncre,
-                                     bool send, int32_t tok, int32_t tj, unsigned long long (&c)[2]) {
+                                     bool send, int32_t tok, int32_t tj, unsigned long long sd,
+                                     unsigned long long (&c)[2]) {
   p.crn[v] = 0;
   const int32_t lo = p.in_off[v];
   uint32_t srt = 0;
   if (send) {
     // SendTokens(v, out-link tj, 1): node.go:112-131
     p.tokens[v] = tok - 1;
-    srt = receive_time(p, send_draw(p, v), t);
+    srt = receive_time(p, sd, t);
   }
   for (int32_t j0 = 0; j0 < od; j0 += R) {
     const int32_t m = od - j0 < R ? od - j0 : R, obc = ob + j0;
@@ -703,7 +707,7 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
 // per-channel FIFO order is the same as one thread pushing them all.
 template <int L>
 __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, int32_t ob, int32_t od, int ncre,
-                                       bool send, int32_t tok, int32_t tj, int32_t jl,
+                                       bool send, int32_t tok, int32_t tj, unsigned long long sd, int32_t jl,
                                        unsigned long long (&c)[2]) {
   if (jl == 0) {
     p.crn[v] = 0;
@@ -727,7 +731,7 @@ __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, i
       push_q(p, ob + j, q, kGMarker | sid, receive_time(p, broadcast_draw(p, s0) + (unsigned long long)j, t), c[0]);
     }
     if (send && j == tj) {
-      push_q(p, ob + j, q, 1u, receive_time(p, send_draw(p, v), t), c[0]);
+      push_q(p, ob + j, q, 1u, receive_time(p, sd, t), c[0]);
       gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[ob + j].x, 1);  // node.go:118
     }
     p.hq[ob + j] = q;
@@ -743,25 +747,34 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
   const int32_t step = sarg >= 0 ? sarg : t;  // the traffic of step t follows tick t
   const int64_t gid = ((int64_t)p.blk_lo * kGThreads * L) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int v = (int)(gid / L), jl = (int)(gid % L);
-  int32_t ob = 0, od = 0, ncre = 0, tok = 0;
+  int32_t ob = 0, od = 0, ncre = 0, tok = 0, tj = -1;
+  bool send = false;
+  uint64_t q0 = 0;
+  unsigned long long sd = 0;
   if (v < p.part_hi) {  // loaded while the status check is in flight
     ob = p.out_off[v];
     od = p.out_off[v + 1] - ob;
     ncre = p.crn[v];
     tok = p.tokens[v];
+    // the traffic decision and what its push reads: the draw index (k_scan's bases, the
+    // block tally) and, for a node without broadcasts, the channel's head word
+    send = traffic_send(p, step, v, od, tok, &tj);
+    if (send) {
+      sd = send_draw(p, v);
+      if (jl == 0) q0 = p.hq[ob + tj];
+    }
   }
   if (block_frozen(p, targ)) return;
   unsigned long long c[2] = {0, 0};  // push, peek
   if (v < p.part_hi) {
-    int32_t tj = -1;
-    const bool send = traffic_send(p, step, v, od, tok, &tj);
     if (ncre) {
-      if constexpr (L == 1) push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, c);
-      else push_node_lanes<L>(p, t, v, ob, od, ncre, send, tok, tj, jl, c);
+      if constexpr (L == 1) push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, sd, c);
+      else push_node_lanes<L>(p, t, v, ob, od, ncre, send, tok, tj, sd, jl, c);
     } else if (send && jl == 0) {
       // SendTokens(v, out-link j, 1): node.go:112-131 (one channel: no batching)
       p.tokens[v] = tok - 1;
-      push_entry(p, ob + tj, 1u, receive_time(p, send_draw(p, v), t), c[0]);
+      push_q(p, ob + tj, q0, 1u, receive_time(p, sd, t), c[0]);
+      p.hq[ob + tj] = q0;
       gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[ob + tj].x, 1);  // node.go:118
     }
   }
