@@ -431,9 +431,6 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   // block's marker count are loaded while the status check is in flight
   const int32_t sendbit = p.part ? 0 : tally_send_bit(p, bk, t);
   const int nm = REMOTE ? min(kGThreads, (int)p.out_n[1] - bk * kGThreads) : p.mcnt[bk];
-  // (the block's marker row too -- its kGThreads slots are allocated whatever nm is)
-  MDel mpre{};
-  if (!REMOTE) mpre = list[threadIdx.x];
   if (REMOTE && nm <= 0) return;
   if (block_frozen(p, targ)) return;
   __shared__ int s_nb, s_base;
@@ -459,7 +456,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   int bslot = -1, cslot = -1;
   BigX bx;
   if ((int)threadIdx.x < nm) {
-    const MDel m = REMOTE ? list[threadIdx.x] : mpre;
+    const MDel m = list[threadIdx.x];  // (not prefetched: C4's blocks mostly have none, 1.2 GB per run)
     const int32_t s0 = m.s0, v = m.v, k = m.k;
     sid = m.sid;
     vdone = v;
