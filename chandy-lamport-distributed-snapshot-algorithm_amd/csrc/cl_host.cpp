@@ -269,6 +269,7 @@ struct cl_sim {
   // replays (cl_rerun: the same program and delays, hence the same queues) run the
   // spill-free kernel.  -1: unknown.
   int64_t nospill_ops = -1;
+  int64_t spill_tried = -1;    // the program length the last probe ran for (no probe twice)
   bool spill_probe = false;    // the last launch was a fresh spill-capable full run (of probe_ops ops)
   int64_t probe_ops = 0;
   // Replays grouped by length: after a fresh full run of ops [0, map_ops) the host orders the
@@ -434,7 +435,7 @@ struct cl_sim {
       if (rc) return rc;
       HIP_TRY(hipMemcpy(d_sched.p, sched.data(), sched.size(), hipMemcpyHostToDevice));
       dev_draws = D;  // longer rows of the same streams: saved draw cursors stay valid
-      nospill_ops = -1;
+      nospill_ops = spill_tried = -1;
       map_ops = map_tried = -1;
       dev_row = D;
       return CL_OK;
@@ -450,7 +451,7 @@ struct cl_sim {
     HIP_TRY(hipMemcpy(d_sched.p, padded.data(), padded.size(), hipMemcpyHostToDevice));
     dev_draws = user_draws;
     dev_row = row;
-    nospill_ops = -1;
+    nospill_ops = spill_tried = -1;
     map_ops = map_tried = -1;
     return CL_OK;
   }
@@ -509,7 +510,7 @@ struct cl_sim {
     if ((rc = d_ovf.ensure(ov))) return rc;
     if ((rc = d_ovh.ensure(lay.ocap_log2 >= 0 ? (size_t)std::max(C, 1) * stride : 1))) return rc;
     if ((rc = d_spilled.ensure(1))) return rc;
-    nospill_ops = -1;  // (a new layout: probe again)
+    nospill_ops = spill_tried = -1;  // (a new layout: probe again)
     map_ops = map_tried = -1;
     need_fresh = true;
     return CL_OK;
@@ -635,7 +636,9 @@ struct cl_sim {
     p.inst_map = begin == 0 && map_ops == (int64_t)ops.size() ? d_map.p : nullptr;
     map_probe = begin == 0 && !p.inst_map && n_inst >= kMapMinInstances && map_tried != (int64_t)ops.size();
     map_probe_ops = (int64_t)ops.size();
-    spill_probe = begin == 0 && trace_n == 0 && !p.nospill && lay.ocap_log2 >= 0;
+    // (a probe clears a device flag with a copy on the stream: once per program, not per
+    // replay -- per replay it put a ~10 us gap between the benchmark's launches)
+    spill_probe = begin == 0 && trace_n == 0 && !p.nospill && lay.ocap_log2 >= 0 && spill_tried != (int64_t)ops.size();
     if (spill_probe) {
       probe_ops = (int64_t)ops.size();
       HIP_TRY(hipMemsetAsync(d_spilled.p, 0, sizeof(uint32_t), stream));
@@ -670,6 +673,7 @@ struct cl_sim {
       uint32_t sp = 1;
       HIP_TRY(hipMemcpy(&sp, d_spilled.p, sizeof sp, hipMemcpyDeviceToHost));
       if (!sp) nospill_ops = probe_ops;
+      spill_tried = probe_ops;
       spill_probe = false;
     }
     if (map_probe) {
@@ -928,7 +932,7 @@ int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks) 
 
 int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
   SIM_CHECK(sim);
-  sim->nospill_ops = -1;
+  sim->nospill_ops = sim->spill_tried = -1;
   sim->map_ops = sim->map_tried = -1;
   sim->go_seeds = true;
   sim->seed_base = seed_base;
@@ -939,7 +943,7 @@ int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
 
 int cl_set_delay_schedule(cl_sim* sim, const uint8_t* delays, int64_t draws_per_instance) {
   SIM_CHECK(sim);
-  sim->nospill_ops = -1;
+  sim->nospill_ops = sim->spill_tried = -1;
   sim->map_ops = sim->map_tried = -1;
   if (!delays || draws_per_instance <= 0) return set_err(CL_E_INVALID, "empty schedule");
   const size_t n = (size_t)(draws_per_instance * sim->n_inst);
