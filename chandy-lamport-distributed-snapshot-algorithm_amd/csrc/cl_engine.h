@@ -262,7 +262,15 @@ struct SumParams {
 //     in[k] = src rank (bits 7..0) | sender's out-index of this channel (15..8) | channel id (31..16)
 //   then init_tok[N] at N * topo_w
 // Launchers (cl_kernels.hip); return hipError_t as int.
-int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream);
+// The exec kernel's stream and its timing events (hipEvent_t, or null): the events are
+// recorded by the dispatch itself (hipExtLaunchKernel), not as packets of their own --
+// two hipEventRecord packets per launch cost 5.7 us of C2's 0.182 ms step.
+struct ExecLaunch {
+  void* stream;
+  void* ev_start;
+  void* ev_stop;
+};
+int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
 int launch_checksums(const SumParams& p, void* stream);
 
 // Snapshot content hash (shared definition with oracle/cl_oracle.c orc_snapshot_hash).

@@ -29,6 +29,7 @@
 // SendTokens node.go:112-131, HandleMarker node.go:149-171, HandleToken node.go:174-185,
 // drain test_common.go:123-137.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "cl_engine.h"
 
@@ -875,7 +876,7 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
 }  // namespace
 
 template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true>
-int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
+int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
   const int32_t wpb = p.lay.wpb;
   const size_t lds = (size_t)p.lay.wave_words * wpb * sizeof(uint32_t);
   if (lds > 64 * 1024) {
@@ -885,15 +886,15 @@ int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, con
   }
   const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
   const unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
-  hipLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>), dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)stream, p,
-                     topo, ops, sched);
+  hipExtLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>), dim3(blocks), dim3(kWave * wpb), lds,
+                        (hipStream_t)L.stream, (hipEvent_t)L.ev_start, (hipEvent_t)L.ev_stop, 0u, p, topo, ops, sched);
   return (int)hipGetLastError();
 }
 
 template <int D>
-int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
+int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
   // The trace build reads delays from HBM (one instantiation per D, debug runs only).
-  if (p.trace_n > 0) return launch_exec_ds<D, false, true>(p, topo, ops, sched, stream);
+  if (p.trace_n > 0) return launch_exec_ds<D, false, true>(p, topo, ops, sched, L);
   if constexpr (unrolled(D)) {
     // staged delay rows and 2 / 4 / 8 LDS ring slots (every automatic choice): the kernel
     // specialized on the column layout, with or without HBM spill rings
@@ -903,10 +904,10 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
       const bool mp = p.inst_map != nullptr;
 #define CLSNAP_SPEC(C)                                                                              \
   case C:                                                                                           \
-    if (sp) return mp ? launch_exec_ds<D, true, false, C, true, true>(p, topo, ops, sched, stream)   \
-                      : launch_exec_ds<D, true, false, C, true, false>(p, topo, ops, sched, stream); \
-    return mp ? launch_exec_ds<D, true, false, C, false, true>(p, topo, ops, sched, stream)          \
-              : launch_exec_ds<D, true, false, C, false, false>(p, topo, ops, sched, stream);
+    if (sp) return mp ? launch_exec_ds<D, true, false, C, true, true>(p, topo, ops, sched, L)   \
+                      : launch_exec_ds<D, true, false, C, true, false>(p, topo, ops, sched, L); \
+    return mp ? launch_exec_ds<D, true, false, C, false, true>(p, topo, ops, sched, L)          \
+              : launch_exec_ds<D, true, false, C, false, false>(p, topo, ops, sched, L);
       switch (p.lay.cap_log2) {
         CLSNAP_SPEC(1)
         CLSNAP_SPEC(2)
@@ -916,8 +917,8 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
 #undef CLSNAP_SPEC
     }
   }
-  return p.lay.x_delay > 0 ? launch_exec_ds<D, true, false>(p, topo, ops, sched, stream)
-                           : launch_exec_ds<D, false, false>(p, topo, ops, sched, stream);
+  return p.lay.x_delay > 0 ? launch_exec_ds<D, true, false>(p, topo, ops, sched, L)
+                           : launch_exec_ds<D, false, false>(p, topo, ops, sched, L);
 }
 
 // Build split (Makefile): this file is compiled once per degree set so the slow large-D
@@ -925,32 +926,32 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
 // kernel and references every launcher; CLSNAP_PART = D instantiates that D only.  Without
 // CLSNAP_PART one translation unit holds every D up to CLSNAP_MAX_D (variant builds).
 #if defined(CLSNAP_PART) && CLSNAP_PART > 0
-template int launch_exec_d<CLSNAP_PART>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+template int launch_exec_d<CLSNAP_PART>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
 #else
 #if defined(CLSNAP_PART)
-extern template int launch_exec_d<1>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
-extern template int launch_exec_d<2>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
-extern template int launch_exec_d<3>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
-extern template int launch_exec_d<4>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
-extern template int launch_exec_d<8>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
-extern template int launch_exec_d<16>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
-extern template int launch_exec_d<32>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
-extern template int launch_exec_d<64>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
-extern template int launch_exec_d<128>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, void*);
+extern template int launch_exec_d<1>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
+extern template int launch_exec_d<2>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
+extern template int launch_exec_d<3>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
+extern template int launch_exec_d<4>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
+extern template int launch_exec_d<8>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
+extern template int launch_exec_d<16>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
+extern template int launch_exec_d<32>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
+extern template int launch_exec_d<64>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
+extern template int launch_exec_d<128>(const ExecParams&, const uint32_t*, const Op*, const uint8_t*, const ExecLaunch&);
 #endif
 // The kernel is instantiated for degree bounds 1, 2, 3, 4, 8, ... CLSNAP_MAX_D.
-int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, void* stream) {
+int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
   const int32_t d = p.lay.od > p.lay.id ? p.lay.od : p.lay.id;  // D must bound every in- and out-degree
-  if (d <= 1) return launch_exec_d<1>(p, topo, ops, sched, stream);
-  if (d <= 2) return launch_exec_d<2>(p, topo, ops, sched, stream);
-  if (d <= 3) return launch_exec_d<3>(p, topo, ops, sched, stream);  // 8nodes (BASELINE config 3)
-  if (d <= 4) return launch_exec_d<4>(p, topo, ops, sched, stream);
+  if (d <= 1) return launch_exec_d<1>(p, topo, ops, sched, L);
+  if (d <= 2) return launch_exec_d<2>(p, topo, ops, sched, L);
+  if (d <= 3) return launch_exec_d<3>(p, topo, ops, sched, L);  // 8nodes (BASELINE config 3)
+  if (d <= 4) return launch_exec_d<4>(p, topo, ops, sched, L);
 #if CLSNAP_MAX_D >= 8
-  if (d <= 8) return launch_exec_d<8>(p, topo, ops, sched, stream);
-  if (d <= 16) return launch_exec_d<16>(p, topo, ops, sched, stream);
-  if (d <= 32) return launch_exec_d<32>(p, topo, ops, sched, stream);
-  if (d <= 64) return launch_exec_d<64>(p, topo, ops, sched, stream);
-  return launch_exec_d<128>(p, topo, ops, sched, stream);
+  if (d <= 8) return launch_exec_d<8>(p, topo, ops, sched, L);
+  if (d <= 16) return launch_exec_d<16>(p, topo, ops, sched, L);
+  if (d <= 32) return launch_exec_d<32>(p, topo, ops, sched, L);
+  if (d <= 64) return launch_exec_d<64>(p, topo, ops, sched, L);
+  return launch_exec_d<128>(p, topo, ops, sched, L);
 #else
   return (int)hipErrorNotSupported;
 #endif
