@@ -76,11 +76,17 @@ PARITY_KEYS = ("instances", "ok", "fatal", "other", "delivered", "snapshot_hash"
                "cut_residual", "final_residual")
 
 
+# Default (steps, warmup) per config: enough untimed launches for the GPU's clocks to settle
+# (C2's 0.18 ms launches measured 0.185 ms per kernel over 3 warmup + 30 timed steps and
+# 0.176 ms over 300 timed steps) and a timed region of >= 50 ms.
+STEP_DEFAULTS = {"c2": (300, 100), "c3": (20, 10)}
+
+
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: per config, STEP_DEFAULTS)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warmup steps (default: per config)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + sorted(GRAPH_CONFIGS))
     ap.add_argument("--graph-nodes", type=int, default=0, help="override the graph size (c4/c5)")
     ap.add_argument("--graph-steps", type=int, default=0, help="override the tick window (c4/c5)")
@@ -92,7 +98,11 @@ def parse_args():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo for rehearsals")
     ap.add_argument("--shared-device", action="store_true",
                     help="every rank on cuda:0 (multi-rank rehearsal on a one-GPU box)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    steps, warmup = STEP_DEFAULTS.get(args.config, (20, 3))
+    args.steps = steps if args.steps is None else args.steps
+    args.warmup = warmup if args.warmup is None else args.warmup
+    return args
 
 
 def init_dist(args, world, local_rank):
