@@ -1119,10 +1119,17 @@ void launch_push(const GParams& p, int32_t t, int32_t step, hipStream_t s) {
 }
 void launch_push(const GParams& p, int32_t t, hipStream_t s) { launch_push(p, t, t, s); }
 
+// k_scan's workgroup: four block tallies per thread, whole waves, at most 1024 threads (C5's
+// 391 blocks scan with two waves: fewer barrier participants on a per-tick latency path)
+static dim3 scan_block(const GParams& p) {
+  const int32_t nb = p.blk_hi - p.blk_lo, th = ((nb + 3) / 4 + 63) & ~63;
+  return dim3((unsigned)(th < 64 ? 64 : th > 1024 ? 1024 : th));
+}
+
 int cg_launch_sends(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_tally, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p, 0, 0, 0);
+  hipLaunchKernelGGL(k_scan, dim3(1), scan_block(p), 0, s, p, 0, 0, 0);
   launch_push(p, t, s);
   return hipGetLastError();
 }
@@ -1131,7 +1138,7 @@ int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   launch_pick(p, dim3(p.n_pblocks), t, s);
   hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p, t, 0, 0);
+  hipLaunchKernelGGL(k_scan, dim3(1), scan_block(p), 0, s, p, t, 0, 0);
   launch_push(p, t, s);
   return hipGetLastError();
 }
@@ -1152,7 +1159,7 @@ int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain,
     const int32_t ta = -1 - (int32_t)((first + i) & 1);
     launch_pick(p, dim3(p.n_pblocks), ta, s);
     hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, ta);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p, ta, n_before, md);
+    hipLaunchKernelGGL(k_scan, dim3(1), scan_block(p), 0, s, p, ta, n_before, md);
     launch_push(p, ta, ta, s);
   }
   return hipGetLastError();
@@ -1201,7 +1208,7 @@ int cg_launch_part_tally(const GParams& p, int32_t step, const int2* rep, int32_
   hipStream_t s = (hipStream_t)stream;
   if (n_rep > 0) hipLaunchKernelGGL(k_part_trig, dim3((n_rep + kGThreads - 1) / kGThreads), dim3(kGThreads), 0, s, p, rep, n_rep);
   if (p.blk_hi > p.blk_lo) hipLaunchKernelGGL(k_tally, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, step);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, p, 0, 0, 0);
+  hipLaunchKernelGGL(k_scan, dim3(1), scan_block(p), 0, s, p, 0, 0, 0);
   return hipGetLastError();
 }
 
