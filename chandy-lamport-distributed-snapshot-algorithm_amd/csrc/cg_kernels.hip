@@ -546,16 +546,17 @@ __global__ void __launch_bounds__(kGThreads) k_tally(GParams p, int32_t step) {
   tally(p, bk, trig, sendbit);
 }
 
-// phase C: exclusive scan of the block tallies (one workgroup, 4 entries per thread),
+// phase C: exclusive scan of the block tallies (one workgroup, PER entries per thread),
 // draw bases
+template <int PER>
 __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t n_before, int32_t max_drain) {
   // the first chunk of block tallies is loaded while the status check is in flight (one
   // latency, not two: this single-workgroup kernel is pure latency, ~6 us per tick)
-  long long pa[4], pb[4];
+  long long pa[PER], pb[PER];
   {
-    const int i0 = p.blk_lo + 4 * threadIdx.x;
+    const int i0 = p.blk_lo + PER * threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < PER; ++q) {
       const bool in = i0 + q < p.blk_hi;
       pa[q] = in ? p.bsum[2 * (i0 + q)] : 0;
       pb[q] = in ? p.bsum[2 * (i0 + q) + 1] : 0;
@@ -567,10 +568,10 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t 
   }
   __shared__ long long sh[32];
   long long carry_a = 0, carry_b = 0;
-  for (int c0 = p.blk_lo; c0 < p.blk_hi; c0 += 4 * blockDim.x) {
-    const int i0 = c0 + 4 * threadIdx.x;
-    long long va[4], vb[4], a = 0, b = 0;
-    for (int q = 0; q < 4; ++q) {
+  for (int c0 = p.blk_lo; c0 < p.blk_hi; c0 += PER * blockDim.x) {
+    const int i0 = c0 + PER * threadIdx.x;
+    long long va[PER], vb[PER], a = 0, b = 0;
+    for (int q = 0; q < PER; ++q) {
       const bool in = i0 + q < p.blk_hi;
       va[q] = c0 == p.blk_lo ? pa[q] : in ? p.bsum[2 * (i0 + q)] : 0;
       vb[q] = c0 == p.blk_lo ? pb[q] : in ? p.bsum[2 * (i0 + q) + 1] : 0;
@@ -581,7 +582,7 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t 
     block_exclusive_scan2(a, b, ta, tb, sh);
     a += carry_a;
     b += carry_b;
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < PER; ++q) {
       if (i0 + q < p.blk_hi) {
         p.bsum[2 * (i0 + q)] = a;
         p.bsum[2 * (i0 + q) + 1] = b;
@@ -1119,17 +1120,23 @@ void launch_push(const GParams& p, int32_t t, int32_t step, hipStream_t s) {
 }
 void launch_push(const GParams& p, int32_t t, hipStream_t s) { launch_push(p, t, t, s); }
 
-// k_scan's workgroup: four block tallies per thread, whole waves, at most 1024 threads (C5's
-// 391 blocks scan with two waves: fewer barrier participants on a per-tick latency path)
-static dim3 scan_block(const GParams& p) {
-  const int32_t nb = p.blk_hi - p.blk_lo, th = ((nb + 3) / 4 + 63) & ~63;
-  return dim3((unsigned)(th < 64 ? 64 : th > 1024 ? 1024 : th));
+// k_scan on a per-tick latency path: up to 512 block tallies (C5: 391) are scanned by one
+// wave, eight per thread; more by whole waves of four per thread, at most 1024 threads
+// (C5 with a 1024-thread workgroup: 5,242 ms per run; 2 waves: 5,038)
+static void launch_scan(const GParams& p, int32_t targ, int32_t n_before, int32_t max_drain, hipStream_t s) {
+  const int32_t nb = p.blk_hi - p.blk_lo;
+  if (nb <= 8 * 64) {
+    hipLaunchKernelGGL(k_scan<8>, dim3(1), dim3(64), 0, s, p, targ, n_before, max_drain);
+    return;
+  }
+  const int32_t th = ((nb + 3) / 4 + 63) & ~63;
+  hipLaunchKernelGGL(k_scan<4>, dim3(1), dim3((unsigned)(th > 1024 ? 1024 : th)), 0, s, p, targ, n_before, max_drain);
 }
 
 int cg_launch_sends(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_tally, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
-  hipLaunchKernelGGL(k_scan, dim3(1), scan_block(p), 0, s, p, 0, 0, 0);
+  launch_scan(p, 0, 0, 0, s);
   launch_push(p, t, s);
   return hipGetLastError();
 }
@@ -1138,7 +1145,7 @@ int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   launch_pick(p, dim3(p.n_pblocks), t, s);
   hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
-  hipLaunchKernelGGL(k_scan, dim3(1), scan_block(p), 0, s, p, t, 0, 0);
+  launch_scan(p, t, 0, 0, s);
   launch_push(p, t, s);
   return hipGetLastError();
 }
@@ -1159,7 +1166,7 @@ int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain,
     const int32_t ta = -1 - (int32_t)((first + i) & 1);
     launch_pick(p, dim3(p.n_pblocks), ta, s);
     hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, ta);
-    hipLaunchKernelGGL(k_scan, dim3(1), scan_block(p), 0, s, p, ta, n_before, md);
+    launch_scan(p, ta, n_before, md, s);
     launch_push(p, ta, ta, s);
   }
   return hipGetLastError();
@@ -1208,7 +1215,7 @@ int cg_launch_part_tally(const GParams& p, int32_t step, const int2* rep, int32_
   hipStream_t s = (hipStream_t)stream;
   if (n_rep > 0) hipLaunchKernelGGL(k_part_trig, dim3((n_rep + kGThreads - 1) / kGThreads), dim3(kGThreads), 0, s, p, rep, n_rep);
   if (p.blk_hi > p.blk_lo) hipLaunchKernelGGL(k_tally, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, step);
-  hipLaunchKernelGGL(k_scan, dim3(1), scan_block(p), 0, s, p, 0, 0, 0);
+  launch_scan(p, 0, 0, 0, s);
   return hipGetLastError();
 }
 
