@@ -35,7 +35,7 @@ constexpr uint32_t kOpen = 0xffffffffu;
 constexpr int32_t kBig = 1 << 30;
 constexpr int32_t kGMaxOutDegree = 64;  // non-empty out-channel bitmask per node (u64)
 constexpr int32_t kGThreads = 256;      // threads (= nodes) per pick / marker / push block
-constexpr int32_t kPushLanes = 8;       // k_push threads per node on small graphs
+constexpr int32_t kPushLanes = 4;       // k_push threads per node on small graphs
 constexpr int32_t kGStatusHistOverflow = 6;
 // A local snapshot created at a node of in-degree above this is expanded over its
 // in-links by the whole k_push grid instead of by the creating lane.

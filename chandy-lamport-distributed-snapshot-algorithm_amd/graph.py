@@ -154,7 +154,7 @@ class GraphSim:
         _check(self._L.cl_graph_set_traffic(self._h, seed, threshold, steps))
 
     def set_push_lanes(self, lanes):
-        """Force the push kernel's lanes per node (0 automatic, 1 or 8): diagnostics and
+        """Force the push kernel's lanes per node (0 automatic, 1 or 4): diagnostics and
         tests -- results are identical on either path."""
         _check(self._L.cl_graph_set_push_lanes(self._h, lanes))
 

@@ -96,8 +96,8 @@ int cl_graph_set_delay_schedule(cl_graph* g, const uint8_t* delays, int64_t n);
  * with out-links sends ONE token when (uint32)cl_counter_hash(seed, k, rank) <
  * threshold, on out-link ((hash >> 32) * outdeg) >> 32 (SendTokens node.go:112-131). */
 int cl_graph_set_traffic(cl_graph* g, uint64_t seed, uint32_t threshold, int64_t steps);
-/* Diagnostic override of the push kernel's lanes per node: 0 = automatic (8 lanes below
- * 2^18 nodes, else 1), 1 or 8 = forced.  Results are identical either way; the tests run
+/* Diagnostic override of the push kernel's lanes per node: 0 = automatic (4 lanes below
+ * 2^18 nodes, else 1), 1 or 4 = forced.  Results are identical either way; the tests run
  * both paths on the same graphs. */
 int cl_graph_set_push_lanes(cl_graph* g, int32_t lanes);
 

@@ -65,7 +65,7 @@ def _worker(rank, world, port, case, out):
 
 
 CASES = [("regular", 4096, 90, 3, 2, 0, False), ("regular", 4096, 100, 5, 3, 1, False),
-         ("powerlaw", 2000, 300, 7, 2, 0, False), ("powerlaw", 2000, 70, 9, 2, 8, True)]
+         ("powerlaw", 2000, 300, 7, 2, 0, False), ("powerlaw", 2000, 70, 9, 2, 4, True)]
 
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}{c[1]}_w{c[4]}_l{c[5]}{'_drain' if c[6] else ''}")
