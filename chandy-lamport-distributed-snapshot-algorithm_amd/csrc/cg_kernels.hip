@@ -422,6 +422,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
 // receivers (k_part_apply's rmlist), 256 per block; their broadcast triggers are reported
 // to the senders' devices.  In the partitioned mode the tally runs after that exchange
 // (k_tally), so k_marker only records the triggers.
+constexpr int32_t kMarkerPrefetchBelow = 1 << 18;
 template <bool REMOTE>
 __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   const int32_t t = tick_time(p, targ);
@@ -432,6 +433,12 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   const int32_t sendbit = p.part ? 0 : tally_send_bit(p, bk, t);
   const int nm = REMOTE ? min(kGThreads, (int)p.out_n[1] - bk * kGThreads) : p.mcnt[bk];
   if (REMOTE && nm <= 0) return;
+  // small graphs (C5: most blocks deliver markers every tick) load the block's marker row
+  // with the status check, one latency off a per-tick chain; large ones (C4: mostly none,
+  // 1.2 GB per run) read it only when it has entries
+  const bool pre = !REMOTE && p.n < kMarkerPrefetchBelow;
+  MDel mpre{};
+  if (pre) mpre = list[threadIdx.x];
   if (block_frozen(p, targ)) return;
   __shared__ int s_nb, s_base;
   __shared__ int s_trig[kGThreads];
@@ -456,7 +463,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   int bslot = -1, cslot = -1;
   BigX bx;
   if ((int)threadIdx.x < nm) {
-    const MDel m = list[threadIdx.x];  // (not prefetched: C4's blocks mostly have none, 1.2 GB per run)
+    const MDel m = pre ? mpre : list[threadIdx.x];
     const int32_t s0 = m.s0, v = m.v, k = m.k;
     sid = m.sid;
     vdone = v;
