@@ -95,6 +95,7 @@ def parse_args():
     ap.add_argument("--fifo-slots", type=int, default=0, help="LDS ring slots per channel (0 = automatic)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-seed first-launch measurement")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo for rehearsals")
     ap.add_argument("--shared-device", action="store_true",
                     help="every rank on cuda:0 (multi-rank rehearsal on a one-GPU box)")
@@ -116,15 +117,21 @@ def init_dist(args, world, local_rank):
 
 
 def profile_entry(cfg, instances):
-    """The matching committed rocprofv3 PMC summary (profiles/<round>_<cfg>_pmc.json)."""
+    """The committed rocprofv3 PMC summary (profiles/<round>_<cfg>_pmc.json) of this
+    per-GPU batch: (path, summary, scale).  The latest round's profile of exactly this
+    many instances, else the latest round's nearest one with its byte and instruction
+    counts scaled by the batch ratio (both are per-instance sums; the resident-wave
+    count is not scaled)."""
     import glob
-    best = None
+    exact, near = None, None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{cfg}_pmc.json"))):
         with open(path) as f:
             d = json.load(f)
         if d.get("instances") == instances:
-            best = (path, d)
-    return best
+            exact = (path, d, 1.0)
+        elif d.get("instances") and (near is None or path.split("_")[0] >= near[0].split("_")[0]):
+            near = (path, d, instances / d["instances"])
+    return exact or near
 
 
 def main():
@@ -169,16 +176,26 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps - 1):
         sim.rerun()
     sim.synchronize()
+    t1 = time.perf_counter()
+    # The last timed step writes into output planes poisoned just before it (outside the
+    # timed region): the parity checksums below can only come from that timed launch.
+    sim.poison_outputs()
+    sim.synchronize()
+    t2 = time.perf_counter()
+    sim.rerun()
+    sim.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = (t1 - t0) + (time.perf_counter() - t2)
     k_total_ms, k_launches = sim.kernel_time()   # HIP events around each timed launch
 
     # checksums of the LAST timed rerun (the timed path itself), all-reduced over ranks
     sums = sim.checksums()
     recorded_ok = sim.counters(only_ok=True)["recorded"]
+    replay = {"slot_map": sim.mapped_replays(), "spill_free_kernel": sim.spill_free_replays()}
+    fresh = fresh_run(cl, per_rank, device, seed_base + total, top, events, args) if not args.no_fresh else None
     t_max, red = cldist.reduce_results(elapsed, sums.tolist() + [recorded_ok], coll_dev)
     tot = dict(zip(cl.SUM_NAMES, red[:len(cl.SUM_NAMES)]))
     tot["recorded"] = red[len(cl.SUM_NAMES)]
@@ -199,9 +216,19 @@ def main():
 
     per_step = t_max / args.steps
     value = delivered_ok / per_step
-    avg_kernel_ms = k_total_ms / max(k_launches, 1)
-    alg = b_alg(counters, n_nodes)                  # bytes per launch (this rank)
+    alg_rank = b_alg(counters, n_nodes)             # bytes per launch (this rank)
+    # whole node: algorithmic bytes of every rank's launch over the slowest rank's average
+    # kernel time, against N x the HBM peak
+    kmax = cldist.reduce_max([k_total_ms / max(k_launches, 1)] +
+                             ([fresh["kernel_ms"]] if fresh else []), coll_dev)
+    avg_kernel_ms = kmax[0]
+    alg = cldist.reduce_results(0.0, [alg_rank], coll_dev)[1][0]
     achieved = alg / (avg_kernel_ms * 1e-3) / 1e9
+    if fresh:
+        fsum = cldist.reduce_results(0.0, [fresh["delivered"]], coll_dev)[1][0]
+        fresh = {"fresh_run_ms": kmax[1], "packets_per_s": fsum / (kmax[1] * 1e-3), "packets": fsum,
+                 "seeds": f"rand.Seed(REFERENCE_SEED + {total} + i): a batch of the same size the "
+                          f"engine never ran", "note": fresh["note"]}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -210,19 +237,23 @@ def main():
     traffic, valu = None, None
     prof = profile_entry(args.config, per_rank)
     if prof is not None and args.fifo_slots == 0:
-        path, d = prof
+        path, d, scale = prof
         c = d["counters"]
+        src = os.path.relpath(path, ROOT) + ("" if scale == 1 else
+                                             f" (x{scale:g}: per-GPU batch {per_rank} vs profiled {d['instances']})")
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            traffic = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+            # whole node, per launch: every rank moves its share
+            traffic = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 * scale * world
         if "SQ_INSTS_VALU" in c:
-            rate = c["SQ_INSTS_VALU"] / (avg_kernel_ms * 1e-3)
-            valu = {"achieved": rate, "peak": VALU_PEAK, "unit": "wave64 VALU instr/s",
-                    "frac": rate / VALU_PEAK, "insts_per_launch": c["SQ_INSTS_VALU"],
-                    "source": os.path.relpath(path, ROOT)}
+            rate = c["SQ_INSTS_VALU"] * scale * world / (avg_kernel_ms * 1e-3)
+            valu = {"achieved": rate, "peak": VALU_PEAK * world, "unit": "wave64 VALU instr/s",
+                    "frac": rate / (VALU_PEAK * world), "insts_per_launch": c["SQ_INSTS_VALU"] * scale * world,
+                    "source": src}
             if "SQ_WAVE_CYCLES" in c and "GRBM_GUI_ACTIVE" in c:
                 # SQ_WAVE_CYCLES counts quad-cycles summed over waves; GRBM over the 8 XCDs
                 valu["waves_per_simd"] = 4 * c["SQ_WAVE_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8) / SIMDS
-    hbm_frac = achieved / HBM_PEAK_GBS
+    peak = HBM_PEAK_GBS * world
+    hbm_frac = achieved / peak
 
     if rank == 0:
         line = {
@@ -248,10 +279,17 @@ def main():
             "checks": {"cut_residual": tot["cut_residual"], "final_residual": tot["final_residual"],
                        "snapshot_hash": tot["snapshot_hash"], "completed": tot["completed"],
                        "recorded": tot["recorded"]},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "fresh_run": fresh,
+            "replay": dict(replay, note="value is the replay rate: the timed steps re-run the same "
+                                        "program and delays, launched through the slot map that the "
+                                        "first run's final ticks give (DESIGN.md section 6); fresh_run is "
+                                        "the first launch on new seeds, with no map"),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": hbm_frac,
                          "traffic": traffic, "kernel": "cl_exec_kernel",
                          "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg,
+                         "scope": f"whole node: {world} GPU(s), bytes summed over ranks, slowest rank's "
+                                  f"average kernel time, peak {world} x {HBM_PEAK_GBS:g} GB/s",
                          "valu": valu,
                          "binding_resource": (
                              "instruction issue per wave-tick at ~5 resident waves per SIMD (LDS-capped): "
@@ -263,6 +301,23 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def fresh_run(cl, n, device, seed_base, top, events, args):
+    """One first launch on seeds the engine never ran: a new batch of the same size and
+    program (instances seeded seed_base + i), no slot map and no spill probe from a prior
+    run -- what a caller with a fresh batch gets.  Warm clocks (it follows the timed
+    region).  Returns its kernel time and the packets its OK instances delivered."""
+    f = cl.ChandyLamportSim(n, device=device, seed_base=seed_base, fifo_lds_slots=args.fifo_slots)
+    f.read_topology_file(os.path.join(TEST_DATA, top))
+    f.read_events_file(os.path.join(TEST_DATA, events))
+    f.rerun()                    # the first launch of this sim: nothing derived from a prior run
+    f.synchronize()
+    ms, launches = f.kernel_time()
+    sums = dict(zip(cl.SUM_NAMES, f.checksums().tolist()))
+    return {"kernel_ms": ms / max(launches, 1), "delivered": sums["delivered"],
+            "note": "first launch of a new sim on unseen seeds (HIP events); not parity-pinned by a "
+                    "fixture -- the same fresh path on the fixture seeds is (tests/test_gpu_parity.py)"}
 
 
 def b_alg_graph(c, n_nodes):
@@ -318,14 +373,22 @@ def bench_graph(args, rank, world, local_rank):
 
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps - 1):
         g.rerun()
     g.synchronize()
+    t1 = time.perf_counter()
+    g.poison_outputs()            # (untimed) the last timed run writes into poisoned planes
+    g.synchronize()
+    t2 = time.perf_counter()
+    g.rerun()
+    g.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = (t1 - t0) + (time.perf_counter() - t2)
     run_ms, runs, ticks = g.run_time()
+    (pre_ms, pre_ticks), (drain_ms, drain_ticks) = g.phase_time()   # the last timed run
     sums = g.checksums()
     status = g.status()
+    parity, parity_ref = graph_parity(args.config, g, rank, n, steps, device)
     vals = [sums[k] for k in clg.GSUM_NAMES]
     t_max, red = cldist.reduce_results(elapsed, vals, coll_dev)
     tot = dict(zip(clg.GSUM_NAMES, red))
@@ -366,6 +429,13 @@ def bench_graph(args, rank, world, local_rank):
                        "snapshots": len(snap_steps), "fifo_slots": fifo,
                        "parallelism": f"one replica per GPU, {world} GPU(s)"},
             "packets_per_step": tot["delivered"],
+            "parity": parity,
+            "parity_ref": parity_ref,
+            "phases": {"traffic": {"ticks": pre_ticks, "ms": pre_ms,
+                                   "us_per_tick": 1e3 * pre_ms / max(pre_ticks, 1)},
+                       "drain": {"ticks": drain_ticks, "ms": drain_ms,
+                                 "us_per_tick": 1e3 * drain_ms / max(drain_ticks, 1)},
+                       "note": "rank 0's last timed run, HIP events at the first drain (cl_graph_phase_time)"},
             "status": {"ok_replicas": tot["ok"], "replicas": world, "rank0_status": status},
             "checks": {"completed": tot["completed"], "cut_residual": tot["cut_residual"],
                        "final_residual": tot["final_residual"], "digest": tot["digest"]},
@@ -378,6 +448,79 @@ def bench_graph(args, rank, world, local_rank):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+GRAPH_FIXTURE = os.path.join(ROOT, "tests", "golden", "graph_runs.json")
+
+
+def _mix64(z):
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    return z ^ (z >> np.uint64(31))
+
+
+def graph_run_summary(g):
+    """The exact run summary tests/graphcheck.py run_summary defines (status, time, counters,
+    completion ticks, content digest of the completed snapshots, final-token sum and hash),
+    from the engine's own results; the fixture holds the CPU oracle's."""
+    c = g.counters()
+    tok = g.node_tokens_array()
+    with np.errstate(over="ignore"):
+        h = int(_mix64(tok.astype(np.uint64) ^ np.arange(tok.size, dtype=np.uint64)).sum(dtype=np.uint64))
+    return {"status": g.status(), "time": g.time(),
+            "counters": {k: c[k] for k in ("push", "peek", "pop_tok", "pop_mk", "recorded", "completed")},
+            "ctick": [g.snapshot_tick(s) for s in range(g.num_snapshots)],
+            "digest_sum": g.checksums()["digest"] % (1 << 64),
+            "final_tokens_sum": int(tok.sum()), "final_tokens_hash": h % (1 << 64)}
+
+
+def fixture_matches(got, want):
+    """Mismatched keys of a run summary against a graph_runs.json summary."""
+    w = dict(want)
+    w["digest_sum"] = sum(want["digest"]) % (1 << 64)
+    w["final_tokens_hash"] = want["final_tokens_hash"] % (1 << 64)
+    return {k: (got[k], w[k]) for k in got if got[k] != w[k]}
+
+
+def graph_parity(cfg, g, rank, n, steps, device):
+    """C4: the timed run itself (rank 0's seeds, the default size) against the CPU oracle's
+    full-size run of the same program.  C5: the full-size run is far beyond the oracle
+    (4e9 deliveries with O(snapshots) recording per token), so the same engine runs the
+    20,000-node x 256-snapshot C5-shape program with the drain against its oracle fixture,
+    after timing; the full-size run is checked by properties in the line's `checks`."""
+    if not os.path.exists(GRAPH_FIXTURE):
+        return None, "no fixture"
+    with open(GRAPH_FIXTURE) as f:
+        runs = json.load(f)["runs"]
+    clg = importlib.import_module(PKG + ".graph")
+    if cfg == "c4":
+        fx = runs.get("c4_full")
+        if rank != 0 or not fx or (fx["nodes"], fx["steps"]) != (n, steps):
+            return None, "the c4_full fixture is rank 0's default-size program"
+        bad = fixture_matches(graph_run_summary(g), fx["summary"])
+        return not bad, ("tests/golden/graph_runs.json c4_full: CPU oracle over the same full-size program "
+                         "(tools/gen_graph_fixture.py), compared with the last timed run (written into "
+                         "poisoned result planes)" + (f"; mismatches {bad}" if bad else ""))
+    fx = runs.get("c5_shape_20k_256")
+    if not fx:
+        return None, "no c5 fixture"
+    m, w, k, seed = fx["nodes"], fx["steps"], fx["snapshots"], 21      # tests/graphcheck.py powerlaw_program
+    s = clg.GraphSim(device=device, fifo_slots=fx["fifo_slots"], max_snapshots=k, max_drain_ticks=fx["max_drain"])
+    s.generate_powerlaw(m, 8, 0.9, True, 100, seed)
+    s.set_delay_hash(seed + 2)
+    s.set_traffic(seed + 1, 1 << 30, w)
+    for step in range(w):
+        if 1 <= step <= k:
+            s.start_snapshot_rank((clg.counter_hash(seed + 3, step - 1, 1) * m) >> 64)
+        s.Tick(1)
+    s.drain()
+    s.flush()
+    bad = fixture_matches(graph_run_summary(s), fx["summary"])
+    return not bad, ("tests/golden/graph_runs.json c5_shape_20k_256: the 20,000-node x 256-snapshot C5-shape "
+                     "program with the drain on the same engine, after timing, vs the CPU oracle's run; the "
+                     "full-size run itself is checked by properties (checks: completed, residuals)"
+                     + (f"; mismatches {bad}" if bad else ""))
 
 
 def cpu_baseline_graph(g, cfg, n, steps, snap_steps, snap_nodes, rs, budget_s):

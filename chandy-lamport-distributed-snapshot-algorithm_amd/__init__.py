@@ -84,6 +84,7 @@ def lib():
         "cl_kernel_time": [vp, vp, vp],
         "cl_replay_spill_free": [vp, vp],
         "cl_replay_mapped": [vp, vp],
+        "cl_debug_poison_outputs": [vp],
         "cl_num_nodes": [vp, vp],
         "cl_node_id": [vp, i32, vp],
         "cl_num_channels": [vp, vp],
@@ -362,6 +363,11 @@ class ChandyLamportSim:
 
     def synchronize(self):
         _check(self._L.cl_synchronize(self._h))
+
+    def poison_outputs(self):
+        """Overwrite every result plane with 0xA5 bytes (cl_debug_poison_outputs): results
+        read after the next rerun() can only come from that launch."""
+        _check(self._L.cl_debug_poison_outputs(self._h))
 
     def last_kernel_ms(self):
         ms = C.c_double(0)

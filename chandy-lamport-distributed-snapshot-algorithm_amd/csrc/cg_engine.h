@@ -123,7 +123,7 @@ struct GScal {
   int32_t dskip[2];
   // parallel send group (k_sg_check -> k_sg_apply)
   int32_t sg_first;              // position of the group's first failing send (INT32_MAX: none)
-  int32_t pad2;
+  int32_t sg_frozen;             // status at the group's start (k_sg_begin): the run was already frozen
   unsigned long long sg_draw0;   // the group's first draw index
   // partitioned mode: this device's tick totals (k_scan), global bases set by the host
   unsigned long long tot_trig, tot_send;

@@ -152,6 +152,10 @@ struct cl_graph {
   size_t ev_used = 0;
   double run_ms = 0;
   int64_t runs = 0, run_ticks = 0, pending_ticks = 0;
+  // phases of the latest run (cl_graph_phase_time): start, first drain, end
+  hipEvent_t ph_ev[3] = {nullptr, nullptr, nullptr};
+  bool ph_drain = false, ph_fresh = false;
+  int64_t ph_time[3] = {0, 0, 0};
 
   GParams P{};
   int32_t s_cap = 0, hist = 0, alloc_cap_log2 = -1;
@@ -209,6 +213,8 @@ struct cl_graph {
       (void)hipEventDestroy(ev.first);
       (void)hipEventDestroy(ev.second);
     }
+    for (auto& e : ph_ev)
+      if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(stream);
   }
 
@@ -652,6 +658,12 @@ struct cl_graph {
     }
     auto& ev = ev_pool[ev_used++];
     GHIP(hipEventRecord(ev.first, stream));
+    for (auto& e : ph_ev)
+      if (!e) GHIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    GHIP(hipEventRecord(ph_ev[0], stream));
+    ph_drain = false;
+    ph_fresh = fresh;
+    ph_time[0] = fresh ? 0 : time;
     size_t begin = executed;
     if (fresh) {
       begin = 0;
@@ -677,11 +689,18 @@ struct cl_graph {
           if ((rc = launch_tick())) return rc;
       } else if (op.kind == P_DRAIN) {
         if ((rc = flush_hostops(pend_begin, pend_count))) return rc;
+        if (!ph_drain) {  // the first drain of the run: the traffic / drain phase boundary
+          GHIP(hipEventRecord(ph_ev[1], stream));
+          ph_drain = true;
+          ph_time[1] = time;
+        }
         if ((rc = run_drain(op.a))) return rc;
       }
     }
     if ((rc = flush_hostops(pend_begin, pend_count))) return rc;
     GHIP(hipEventRecord(ev.second, stream));
+    GHIP(hipEventRecord(ph_ev[2], stream));
+    ph_time[2] = time;
     gop_cursor = pend_begin;
     executed = prog.size();
     state_valid = true;
@@ -1188,6 +1207,40 @@ int cl_graph_run_time(cl_graph* g, double* total_ms, int64_t* runs, int64_t* tic
   return g->fold_time(total_ms, runs, ticks);
 }
 
+int cl_graph_debug_poison_outputs(cl_graph* g) {
+  G_CHECK(g);
+  if (!g->dev_ready || !g->d_tokens.p) return CL_OK;
+  GHIP(hipSetDevice(g->device));
+  GHIP(hipMemsetAsync(g->d_tokens.p, 0xA5, g->d_tokens.bytes(), g->stream));
+  GHIP(hipMemsetAsync(g->d_stok.p, 0xA5, g->d_stok.bytes(), g->stream));
+  GHIP(hipMemsetAsync(g->d_rec.p, 0xA5, g->d_rec.bytes(), g->stream));
+  GHIP(hipMemsetAsync(g->d_ctick.p, 0xA5, g->d_ctick.bytes(), g->stream));
+  GHIP(hipMemsetAsync(g->d_cpart.p, 0xA5, g->d_cpart.bytes(), g->stream));
+  return CL_OK;
+}
+
+int cl_graph_phase_time(cl_graph* g, double* ms, int64_t* ticks) {
+  G_CHECK(g);
+  if (!ms || !ticks) return gerr(CL_E_INVALID, "null output");
+  if (!g->ph_ev[2]) return gerr(CL_E_STATE, "nothing has run");
+  int rc = g->sync();
+  if (rc) return rc;
+  float a = 0.f, b = 0.f;
+  if (g->ph_drain) {
+    GHIP(hipEventElapsedTime(&a, g->ph_ev[0], g->ph_ev[1]));
+    GHIP(hipEventElapsedTime(&b, g->ph_ev[1], g->ph_ev[2]));
+    ticks[0] = g->ph_time[1] - g->ph_time[0];
+    ticks[1] = g->ph_time[2] - g->ph_time[1];
+  } else {
+    GHIP(hipEventElapsedTime(&a, g->ph_ev[0], g->ph_ev[2]));
+    ticks[0] = g->ph_time[2] - g->ph_time[0];
+    ticks[1] = 0;
+  }
+  ms[0] = a;
+  ms[1] = b;
+  return CL_OK;
+}
+
 int cl_graph_device_bytes(cl_graph* g, int64_t* bytes) {
   G_CHECK(g);
   if (!bytes) return gerr(CL_E_INVALID, "null output");
@@ -1527,6 +1580,20 @@ int cl_graph_part_tally(cl_graph* g, int32_t step, const int32_t* reports, int64
   GHIP(hipStreamSynchronize(g->stream));
   totals[0] = (int64_t)sc.tot_trig;
   totals[1] = (int64_t)sc.tot_send;
+  totals[2] = sc.status;
+  return CL_OK;
+}
+
+int cl_graph_part_freeze(cl_graph* g, int32_t status) {
+  G_CHECK(g);
+  G_PART(g);
+  if (status <= 0) return gerr(CL_E_INVALID, "freeze needs a nonzero status");
+  GScal sc;
+  GHIP(hipMemcpyAsync(&sc, g->d_sc.p, sizeof sc, hipMemcpyDeviceToHost, g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  if (sc.status) return CL_OK;
+  GHIP(hipMemcpyAsync(&g->d_sc.p->status, &status, sizeof status, hipMemcpyHostToDevice, g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
   return CL_OK;
 }
 

@@ -920,10 +920,13 @@ __device__ inline int send_check(const GParams& p, const GOp& op, int32_t* c) {
   return 0;
 }
 
+// Both kernels gate on sg_frozen, the status k_sg_begin saw, never on the live status: the
+// group's own first failure sets the status while other blocks of k_sg_apply still have to
+// run the sends before it.
 __global__ void __launch_bounds__(kGThreads) k_sg_check(GParams p, int32_t ob, int32_t oc) {
   const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
   if (i == 0) p.sc->sg_draw0 = p.sc->draw;
-  if (i >= oc || p.sc->status) return;
+  if (i >= oc || p.sc->sg_frozen) return;
   int32_t c;
   if (send_check(p, p.ops[ob + i], &c)) atomicMin(&p.sc->sg_first, i);
 }
@@ -931,7 +934,7 @@ __global__ void __launch_bounds__(kGThreads) k_sg_check(GParams p, int32_t ob, i
 __global__ void __launch_bounds__(kGThreads) k_sg_apply(GParams p, int32_t time, int32_t ob, int32_t oc) {
   const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
   unsigned long long pushes = 0;
-  if (p.sc->status == 0 && i < oc) {
+  if (p.sc->sg_frozen == 0 && i < oc) {
     const int32_t first = p.sc->sg_first;
     const unsigned long long d0 = p.sc->sg_draw0;
     if (i == 0) p.sc->draw = d0 + (unsigned long long)(first < oc ? first : oc);  // draws of the sends that ran
@@ -1189,7 +1192,10 @@ int cg_launch_hostops(const GParams& p, int32_t time, int32_t op_begin, int32_t 
   return hipGetLastError();
 }
 
-__global__ void k_sg_begin(GParams p) { p.sc->sg_first = 0x7fffffff; }
+__global__ void k_sg_begin(GParams p) {
+  p.sc->sg_first = 0x7fffffff;
+  p.sc->sg_frozen = p.sc->status;
+}
 
 int cg_launch_sendgroup(const GParams& p, int32_t time, int32_t op_begin, int32_t op_count, void* stream) {
   hipStream_t s = (hipStream_t)stream;

@@ -177,7 +177,18 @@ struct cl_sim {
   // test_common.go:106-108); `executed_cv` is signalled after every execution.
   mutable std::recursive_mutex mu;
   std::condition_variable_any executed_cv;
-  uint64_t exec_gen = 0;  // executions completed (flushes that ran ops)
+  uint64_t exec_gen = 0;  // executions completed (flushes that ran ops) and ticks issued
+  int32_t waiters = 0;    // threads blocked in cl_wait_snapshot
+  bool closing = false;   // cl_sim_destroy has begun: waiters leave with CL_E_STATE
+
+  // A tick or drain was issued: a waiter re-checks (its check executes the pending events),
+  // so a driver that only calls Tick() -- the reference pattern -- still wakes a blocked
+  // CollectSnapshot (sim.go:137-140).
+  void notify_waiters() {
+    if (!waiters) return;
+    ++exec_gen;
+    executed_cv.notify_all();
+  }
 
   int64_t n_inst = 0;
   int64_t stride = 0;  // n_inst rounded up to the wave size
@@ -838,8 +849,13 @@ int cl_sim_create(int64_t n_instances, cl_sim** out) {
 
 int cl_sim_destroy(cl_sim* sim) {
   if (sim) {
-    sim->mu.lock();  // no other thread may still be inside a call on this sim
-    sim->mu.unlock();
+    // wake every thread blocked in cl_wait_snapshot and wait until it has left; no other
+    // call may be in flight or start on this sim once destroy is called
+    std::unique_lock<std::recursive_mutex> lk(sim->mu);
+    sim->closing = true;
+    ++sim->exec_gen;
+    sim->executed_cv.notify_all();
+    sim->executed_cv.wait(lk, [&] { return sim->waiters == 0; });
   }
   delete sim;
   return CL_OK;
@@ -1003,9 +1019,11 @@ int cl_tick(cl_sim* sim, int32_t n) {
   sim->time_bound += n;
   if (!sim->ops.empty() && sim->ops.back().kind == OP_TICK && sim->executed < (int32_t)sim->ops.size()) {
     sim->ops.back().a += n;  // merge consecutive ticks of one pending run
-    return CL_OK;
+  } else if ((rc = sim->append(Op{OP_TICK, n, 0, 0}))) {
+    return rc;
   }
-  return sim->append(Op{OP_TICK, n, 0, 0});
+  sim->notify_waiters();
+  return CL_OK;
 }
 
 int cl_drain(cl_sim* sim) {
@@ -1017,7 +1035,9 @@ int cl_drain(cl_sim* sim) {
   if (room < 0) return set_err(CL_E_LIMIT, "simulated time would exceed %d ticks", kMaxTime);
   const int64_t cap = std::min(sim->max_drain, room);
   sim->time_bound += cap + extra;
-  return sim->append(Op{OP_DRAIN, (int32_t)cap, (int32_t)extra, 0});
+  if ((rc = sim->append(Op{OP_DRAIN, (int32_t)cap, (int32_t)extra, 0}))) return rc;
+  sim->notify_waiters();
+  return CL_OK;
 }
 
 int cl_read_events_text(cl_sim* sim, const char* text, int32_t* n_snapshots) {
@@ -1089,6 +1109,20 @@ int cl_replay_mapped(cl_sim* sim, int32_t* on) {
 int cl_synchronize(cl_sim* sim) {
   SIM_CHECK(sim);
   return sim->sync();
+}
+
+int cl_debug_poison_outputs(cl_sim* sim) {
+  SIM_CHECK(sim);
+  if (!sim->dev_ready || !sim->d_regs.p) return CL_OK;
+  HIP_TRY(hipSetDevice(sim->device));
+  const int n = (int)sim->ids.size();
+  const size_t nod = (size_t)sim->s_cap * n * sim->lay.rw * sim->stride;
+  HIP_TRY(hipMemsetAsync(sim->d_snap_nod.p, 0xA5, nod * sizeof(uint32_t), sim->stream));
+  HIP_TRY(hipMemsetAsync(sim->d_snap_tick.p, 0xA5, (size_t)sim->s_cap * sim->stride * sizeof(int32_t), sim->stream));
+  HIP_TRY(hipMemsetAsync(sim->d_regs.p, 0xA5, (size_t)R_NUM * sim->stride * sizeof(int32_t), sim->stream));
+  HIP_TRY(hipMemsetAsync(sim->d_fin_tok.p, 0xA5, (size_t)n * sim->stride * sizeof(int32_t), sim->stream));
+  sim->h_valid = false;
+  return CL_OK;
 }
 
 int cl_last_kernel_ms(cl_sim* sim, double* ms) {
@@ -1256,7 +1290,15 @@ int cl_wait_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi,
   if (sid < 0 || sid >= sim->n_sids || inst_lo < 0 || inst_hi > sim->n_inst || inst_lo > inst_hi)
     return set_err(CL_E_INVALID, "snapshot/instance range out of range");
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
+  struct Waiting {  // registered while blocked, so cl_sim_destroy can wait for this thread
+    cl_sim* s;
+    explicit Waiting(cl_sim* x) : s(x) { ++s->waiters; }
+    ~Waiting() {
+      if (--s->waiters == 0 && s->closing) s->executed_cv.notify_all();
+    }
+  } waiting(sim);
   for (;;) {
+    if (sim->closing) return set_err(CL_E_STATE, "the sim is being destroyed");
     int64_t n = 0, frozen = 0;
     int rc = sim->count_complete(sid, inst_lo, inst_hi, &n, &frozen);
     if (rc) return rc;

@@ -27,6 +27,14 @@ def reduce_results(elapsed_s, sums, device):
     return float(t.item()), [int(v) for v in s.tolist()]
 
 
+def reduce_max(values, device):
+    """Elementwise max of float values over all ranks."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
+
+
 # ---- exchange layer of the graph-partitioned mode (DESIGN.md §11) ---------------------
 # One simulation whose nodes are split into rank ranges exchanges, every tick, records
 # addressed to the owners of other nodes (deliveries, broadcast-trigger reports, draw

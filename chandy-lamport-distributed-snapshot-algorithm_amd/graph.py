@@ -62,6 +62,8 @@ def glib():
             "cl_graph_rerun": [vp],
             "cl_graph_synchronize": [vp],
             "cl_graph_run_time": [vp, vp, vp, vp],
+            "cl_graph_phase_time": [vp, vp, vp],
+            "cl_graph_debug_poison_outputs": [vp],
             "cl_graph_device_bytes": [vp, vp],
             "cl_graph_get_status": [vp, vp],
             "cl_graph_get_time": [vp, vp],
@@ -78,6 +80,7 @@ def glib():
             "cl_graph_part_tally": [vp, i32, vp, i64, vp],
             "cl_graph_part_bases": [vp, vp, vp, i64, vp],
             "cl_graph_part_push": [vp, i32, vp, i64],
+            "cl_graph_part_freeze": [vp, i32],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -211,6 +214,17 @@ class GraphSim:
         ms, r, t = C.c_double(0), C.c_int64(0), C.c_int64(0)
         _check(self._L.cl_graph_run_time(self._h, C.byref(ms), C.byref(r), C.byref(t)))
         return ms.value, r.value, t.value
+
+    def poison_outputs(self):
+        """Overwrite the result planes with 0xA5 bytes (cl_graph_debug_poison_outputs)."""
+        _check(self._L.cl_graph_debug_poison_outputs(self._h))
+
+    def phase_time(self):
+        """Latest run: ((ms, ticks) before the first drain, (ms, ticks) of the drains)."""
+        ms = np.zeros(2, dtype=np.float64)
+        t = np.zeros(2, dtype=np.int64)
+        _check(self._L.cl_graph_phase_time(self._h, _p(ms), _p(t)))
+        return (float(ms[0]), int(t[0])), (float(ms[1]), int(t[1]))
 
     # ---- queries ------------------------------------------------------------------------
     def _get(self, fn, ctype, *args):
@@ -358,6 +372,7 @@ class PartitionedGraphSim:
         _check(self._L.cl_graph_part_begin(sim._h, self.lo, self.hi))
         self.time = 0
         self.n_sids = 0
+        self.frozen = 0
 
     def owner(self, v):
         return np.asarray(v) // self.span
@@ -373,9 +388,15 @@ class PartitionedGraphSim:
         step-0 traffic with no reports)."""
         mine = np.concatenate([r for r in reports_by_src if len(r)] or [np.zeros((0, 2), dtype=np.int64)])
         rep = np.ascontiguousarray(mine, dtype=np.int32)
-        tot = np.zeros(2, dtype=np.int64)
+        tot = np.zeros(3, dtype=np.int64)
         _check(self._L.cl_graph_part_tally(self.g._h, step, _p(rep), len(rep), _p(tot)))
         allt = self.D.allgather_ints(tot.tolist(), self.dev)
+        frozen = int(allt[:, 2].max())
+        if frozen:                  # a device froze (its totals are stale): every device stops here
+            if not tot[2]:
+                _check(self._L.cl_graph_part_freeze(self.g._h, frozen))
+            self.frozen = frozen
+            return
         r = self.rank
         bases = np.array([allt[:r, 0].sum(), allt[:, 0].sum(), allt[:r, 1].sum(), allt[:, 1].sum()], dtype=np.int64)
         s0 = np.ascontiguousarray(rep[:, 0]) if len(rep) else np.zeros(0, dtype=np.int32)
@@ -403,6 +424,8 @@ class PartitionedGraphSim:
         return sid.value
 
     def tick(self):                                 # sim.go:71-95 across the ranks
+        if self.frozen:                             # (the run stopped on every rank)
+            return
         h = self.g._h
         out = np.zeros((max(self.hi - self.lo, 1), 4), dtype=np.int32)
         m = C.c_int64(0)
@@ -439,6 +462,8 @@ class PartitionedGraphSim:
         """test_common.go:123-137 across the ranks: tick until every snapshot started so far
         has completed on every rank, then maxDelay + 1 more ticks."""
         for _ in range(max_ticks + 1):
+            if self.frozen:
+                return False
             if all(x >= 0 for x in self.completion_ticks()):
                 for _ in range(6):
                     self.tick()

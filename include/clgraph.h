@@ -124,6 +124,15 @@ int cl_graph_synchronize(cl_graph* g);
 /* Device time of the runs since the previous call (HIP events on the engine stream
  * around each flush / rerun), the number of runs, and the ticks they executed. */
 int cl_graph_run_time(cl_graph* g, double* total_ms, int64_t* runs, int64_t* ticks);
+/* Test/benchmark aid: overwrite the run's result planes (node tokens, snapshot token maps
+ * and cursors, completion ticks, counters) with 0xA5 bytes on the engine's stream, so
+ * results read after the next cl_graph_rerun come from that run alone. */
+int cl_graph_debug_poison_outputs(cl_graph* g);
+/* Phases of the latest run: ms[0] / ticks[0] from its start to its first drain (the event
+ * program's ticks: the traffic window of the synthetic workloads), ms[1] / ticks[1] the
+ * drains (test_common.go:123-137); ms[1] = ticks[1] = 0 without a drain.  HIP events on the
+ * engine's stream. */
+int cl_graph_phase_time(cl_graph* g, double* ms /* [2] */, int64_t* ticks /* [2] */);
 int cl_graph_device_bytes(cl_graph* g, int64_t* bytes);
 
 /* ---- results (flush pending events first) ----------------------------------- */
@@ -167,7 +176,11 @@ int cl_graph_trace_read(cl_graph* g, cl_log_event* out, int32_t cap, int32_t* n_
  *                 nodes, any order), handles the markers (node.go:149-171); returns the
  *                 broadcast triggers of other devices' senders, rows (s0, outdeg).
  *   part_tally    applies the reports addressed here, tallies triggers and next-step sends
- *                 of the owned senders; totals[0..1] = (trigger draws, send draws).
+ *                 of the owned senders; totals[0..2] = (trigger draws, send draws, this
+ *                 device's run status).  A device that froze (engine limit) tallies
+ *                 nothing, so the caller allgathers the status with the totals and, when
+ *                 any device has one, freezes every device (part_freeze) before part_bases:
+ *                 no device then draws from stale totals.
  *   part_bases    bases[4] = (trigger draws of lower devices, of all, send draws of lower
  *                 devices, of all); returns the first draw of each reported sender s0.
  *   part_push     replies (s0, draw0) for broadcasts triggered by other devices' senders;
@@ -185,6 +198,9 @@ int cl_graph_part_receive(cl_graph* g, const int32_t* rows, int64_t n, int32_t* 
 int cl_graph_part_tally(cl_graph* g, int32_t step, const int32_t* reports, int64_t n, int64_t* totals);
 int cl_graph_part_bases(cl_graph* g, const int64_t* bases, const int32_t* s0, int64_t n, int64_t* draw0);
 int cl_graph_part_push(cl_graph* g, int32_t step, const int64_t* replies, int64_t n);
+/* Freeze this device's part of the run with `status` (no-op if it is already frozen):
+ * another device froze, and the partitioned run stops everywhere at the same step. */
+int cl_graph_part_freeze(cl_graph* g, int32_t status);
 
 /* ---- counter hash of the synthetic workloads ------------------------------------ */
 uint64_t cl_counter_hash(uint64_t seed, uint64_t a, uint64_t b);

@@ -91,6 +91,8 @@ typedef struct cl_sim cl_sim;
 
 /* NewSimulator (sim.go:28-37) for n_instances independent instances. No GPU work. */
 int cl_sim_create(int64_t n_instances, cl_sim** out);
+/* Wakes every thread blocked in cl_wait_snapshot (they return CL_E_STATE) and waits for
+ * them to leave before freeing the sim; no other call may overlap it. */
 int cl_sim_destroy(cl_sim* sim);
 
 /* AddNode (sim.go:40-43; node.go:45-55). Token counts must fit int32 in total. */
@@ -151,6 +153,12 @@ int cl_replay_spill_free(cl_sim* sim, int32_t* on);
  * instances sharing a wave finish together; engine-internal, results unchanged). */
 int cl_replay_mapped(cl_sim* sim, int32_t* on);
 
+/* Test/benchmark aid (no reference counterpart): overwrite every result plane the exec
+ * kernel writes -- node snapshot records, completion ticks, per-instance result rows,
+ * final node tokens -- with the byte 0xA5 on the sim's stream, so that results read after
+ * the next cl_rerun can only come from that launch.  No-op before the first execution. */
+int cl_debug_poison_outputs(cl_sim* sim);
+
 /* ---- topology queries (host only) ---------------------------------------- */
 int cl_num_nodes(const cl_sim* sim, int32_t* n);
 int cl_node_id(const cl_sim* sim, int32_t rank, const char** id); /* owned by sim */
@@ -185,8 +193,9 @@ int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens,
 int cl_poll_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t* n_complete);
 /* The blocking side of CollectSnapshot (sim.go:137-140): wait until snapshot sid has
  * completed in every instance of [inst_lo, inst_hi).  The caller is a collector thread;
- * it is woken after each execution of the driver's events (cl_flush, queries) and
- * re-checks.  timeout_ms < 0 waits forever; on timeout returns CL_E_NOT_COMPLETE with
+ * it is woken after each execution of the driver's events (cl_flush, queries) and after
+ * every cl_tick / cl_drain, and re-checks (executing the pending events itself, so a
+ * driver that only calls Tick() -- the reference's pattern -- completes the wait).  timeout_ms < 0 waits forever; on timeout returns CL_E_NOT_COMPLETE with
  * *n_complete (may be NULL) set.  It also returns CL_E_NOT_COMPLETE at once when every
  * instance of the range has either completed or stopped with a non-OK status (the
  * reference process would have exited at that log.Fatal; such an instance never

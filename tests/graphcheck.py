@@ -55,6 +55,27 @@ def powerlaw_program(n, steps, n_snaps, seed=21, **kw):
                    traffic_steps=steps, snap_step=ss, snap_rank=sr, delay_seed=seed + 2, **kw)
 
 
+def bench_program(cfg_name, rank=0):
+    """bench.py's graph program for one rank (GRAPH_CONFIGS: same graph, seeds and snapshot
+    placement; the graph as the engine's host generator builds it, which tests/test_graph_
+    host.py pins against graphgen's restatement)."""
+    import bench
+    cfg = bench.GRAPH_CONFIGS[cfg_name]
+    n, steps = cfg["n"], cfg["steps"]
+    snap_steps = [k for k in cfg["snap_steps"] if k < steps]
+    rs = cfg["seed"] + 1000 * rank
+    snap_nodes = [G.mulhi(G.counter_hash(rs + 3, i, 1), n) for i in range(len(snap_steps))]
+    g = clg.GraphSim()
+    if cfg["kind"] == "regular":
+        g.generate_regular(n, cfg["degree"], cfg["tokens"], cfg["seed"])
+    else:
+        g.generate_powerlaw(n, cfg["targets"], cfg["exponent"], cfg["ring"], cfg["tokens"], cfg["seed"])
+    src, dst = g.channels()
+    return Program(np.full(n, cfg["tokens"]), src, dst, steps, traffic_seed=rs + 2, thresh=1 << 30,
+                   traffic_steps=steps, snap_step=snap_steps, snap_rank=snap_nodes, delay_seed=rs + 1,
+                   fifo_slots=cfg["fifo"]), cfg
+
+
 def _snaps(n, snaps, seed):
     ss, sr = [], []
     for i, (step, rank) in enumerate(snaps):

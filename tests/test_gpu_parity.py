@@ -245,7 +245,9 @@ def test_rerun_equals_flush_and_oracle(cfg):
     """The benchmark's timed path: cl_rerun replays the program from the initial state
     with the kernel prologue resetting completion ticks and HBM spill-ring heads (no fill
     launch).  Three reruns after the first flush must reproduce the flush and the oracle
-    exactly -- statuses, times, batch checksums, and sampled instances in full."""
+    exactly -- statuses, times, batch checksums, and sampled instances in full.  Every
+    output plane is poisoned before each rerun, so a rerun that skipped (or only partly
+    made) its stores would fail."""
     top, events, n, slots = cfg
     sim = engine_run(top, events, n, fifo_lds_slots=slots)
     first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
@@ -257,7 +259,13 @@ def test_rerun_equals_flush_and_oracle(cfg):
         assert not sim.mapped_replays()
     _, st, ticks, cnt, hashes = oracle_batch(top, events, n, threads=16)
     want = batch_sums_from_oracle(st, cnt, hashes)
+    # the poison reaches every plane the results are read from: without a rerun, nothing
+    # the flush wrote survives
+    sim.poison_outputs()
+    assert not np.array_equal(sim.checksums(), first[2])
+    assert not np.array_equal(sim.status(), first[0]) and not np.array_equal(sim.time(), first[1])
     for r in range(3):
+        sim.poison_outputs()      # results below can only come from this rerun
         sim.rerun()
         sim.synchronize()
         status, times, sums = sim.status(), sim.time(), sim.checksums()
@@ -293,6 +301,7 @@ def test_spill_free_replay_after_probe():
     for i in range(0, n, 37):
         compare_instance(sim, i, oracle_run(top, ev, seed=O.REFERENCE_SEED + i), status=first[0], times=first[1])
     for _ in range(2):
+        sim.poison_outputs()
         sim.rerun()
         sim.synchronize()
         assert np.array_equal(sim.status(), first[0]) and np.array_equal(sim.time(), first[1])
@@ -314,7 +323,8 @@ def test_spill_free_replay_after_probe():
 def test_headline_batch_2p20_matches_fixture():
     """The north_star batch itself (BASELINE config 3, 2^20 instances on one GPU): the
     batch checksums of a flush and of a rerun equal the oracle's values over every
-    instance (tests/golden/bench_sums.json, tools/gen_bench_fixture.py)."""
+    instance (tests/golden/bench_sums.json, tools/gen_bench_fixture.py); the rerun's outputs
+    are poisoned beforehand, so they come from the rerun alone."""
     import json
     fx = json.load(open(os.path.join(os.path.dirname(TEST_DATA), "bench_sums.json")))
     want = fx["batches"]["c3"]["sums"]
@@ -326,6 +336,7 @@ def test_headline_batch_2p20_matches_fixture():
         got["recorded"] = sim.counters(only_ok=True)["recorded"]
         for k in want:
             assert (got[k] - want[k]) % (1 << 64) == 0, f"pass {rnd} {k}: engine {got[k]} vs oracle {want[k]}"
+        sim.poison_outputs()      # the next pass reads only what the rerun wrote
         sim.rerun()
         sim.synchronize()
 
@@ -358,6 +369,7 @@ def test_two_event_texts_and_snapshot_after_drain():
                 o.tick()
         refs.append(o)
         compare_instance(sim, i, o, status=first[0], times=first[1])
+    sim.poison_outputs()
     sim.rerun()
     sim.synchronize()
     assert np.array_equal(sim.status(), first[0]) and np.array_equal(sim.time(), first[1])

@@ -5,9 +5,11 @@ reference-level counters (pushes = delay draws, peeks, delivered tokens / marker
 recorded copies, completed snapshots).
 
 At BASELINE config 4's full size (2^20-node regular digraph, one snapshot under
-continuous traffic) the run is checked through size-independent properties: the
-snapshot completes, its cut is consistent (snapshot tokens + recorded messages =
-total), final tokens + in-flight tokens = total, and reruns are deterministic.
+continuous traffic) the benchmark's exact program is compared with the CPU oracle's
+full-size run (tests/golden/graph_runs.json c4_full), and checked through
+size-independent properties: the snapshot completes, its cut is consistent (snapshot
+tokens + recorded messages = total), final tokens + in-flight tokens = total, and
+reruns into poisoned result planes reproduce the run.
 """
 import os
 
@@ -138,6 +140,47 @@ def test_random_host_events_vs_oracle(seed):
     n = int(rng.integers(2, 30))
     src, dst = _random_graph(rng, n)
     _random_events_run(rng, n, src, dst, O.REFERENCE_SEED + seed, int(rng.integers(5, 40)))
+
+
+@pytest.mark.parametrize("kind", ["insufficient", "unknown_dest", "none"])
+def test_large_send_group_with_late_fatal_vs_oracle(kind):
+    """A run of 700 sends from pairwise distinct senders executes as one parallel send
+    group over three 256-thread blocks (k_sg_check / k_sg_apply).  The first failing send
+    (program order) sits in the last block: every earlier send must run, none after it,
+    and the draw index must advance by exactly the sends that ran (node.go:112-131,
+    sim.go:101) -- however the blocks are scheduled."""
+    n = 720
+    rng = np.random.default_rng(41)
+    ids = [f"v{r:03d}" for r in range(n)]
+    tok = [5] * n
+    order = [int(x) for x in rng.permutation(n)[:700]]
+    bad = order[600]
+    if kind == "insufficient":
+        tok[bad] = 0
+    top = f"{n}\n" + "".join(f"{ids[r]} {tok[r]}\n" for r in range(n)) + \
+        "".join(f"{ids[r]} {ids[(r + 1) % n]}\n{ids[r]} {ids[(r - 1) % n]}\n" for r in range(n))
+    ev = ["tick"]
+    for v in order:
+        dest = ids[(v + 1) % n]
+        if kind == "unknown_dest" and v == bad:
+            dest = ids[(v + 7) % n]             # no such link
+        ev.append(f"send {ids[v]} {dest} 1")
+    ev += ["snapshot v000", "tick 3"] + [f"send {ids[v]} {ids[(v - 1) % n]} 1" for v in order[:300]] + ["tick 2"]
+    events = "\n".join(ev) + "\n"
+    gseed = O.REFERENCE_SEED + 5
+    o = O.OracleSim()
+    o.seed_go(gseed)
+    assert o.read_topology_text(top) == 0
+    o.read_events_text(events, 2000)
+    want = {"insufficient": 1, "unknown_dest": 2, "none": 0}[kind]
+    assert o.status == want
+    for _ in range(3):                           # (block scheduling varies run to run)
+        g = clg.GraphSim(max_drain_ticks=2000)
+        g.read_topology_text(top)
+        g.set_delay_go_seed(gseed)
+        g.read_events_text(events)
+        g.flush()
+        compare(g, o)
 
 
 @pytest.mark.parametrize("lanes", [0, 1, 4])
@@ -314,6 +357,39 @@ def test_c4_full_size_properties():
     assert g.checksums() == sums
 
 
+def test_c4_full_size_bench_program_vs_oracle_fixture():
+    """BASELINE config 4 exactly as bench.py runs it (2^20 nodes, 8-out regular digraph
+    from the engine's generator, 80 ticks of traffic, one snapshot at step 5, rank 0's
+    seeds): the engine's run summary -- status, time, push / peek / delivered / recorded
+    / completed counters, completion tick, snapshot content digest, final token sum and
+    hash -- equals the CPU oracle's full-size run (tests/golden/graph_runs.json c4_full,
+    tools/gen_graph_fixture.py; sim.go:71-95, node.go:149-185 at scale).  A rerun into
+    poisoned result planes must reproduce it too (the benchmark's timed path)."""
+    import json
+    from graphcheck import bench_program
+    from snapcheck import ROOT
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "graph_runs.json")))["runs"]["c4_full"]
+    p, cfg = bench_program("c4")
+    assert (p.n, p.steps, len(p.snap_step)) == (fx["nodes"], fx["steps"], fx["snapshots"])
+    g = clg.GraphSim(fifo_slots=cfg["fifo"], max_snapshots=1, max_drain_ticks=1_000_000)
+    g.generate_regular(p.n, cfg["degree"], cfg["tokens"], cfg["seed"])     # bench.py's own path
+    g.set_delay_hash(p.delay_seed)
+    g.set_traffic(p.traffic_seed, p.thresh, p.traffic_steps)
+    for k in range(p.steps):
+        if k in p.snap_step:
+            g.start_snapshot_rank(int(p.snap_rank[list(p.snap_step).index(k)]))
+        g.Tick(1)
+    g.flush()
+    want = fx["summary"]
+    for rnd in range(2):
+        got = engine_summary(g)
+        for k in want:
+            assert got[k] == want[k], f"pass {rnd} {k}: engine {got[k]} vs oracle {want[k]}"
+        g.poison_outputs()
+        g.rerun()
+        g.synchronize()
+
+
 @pytest.mark.parametrize("lanes", [1, 4])
 def test_powerlaw_with_drain_vs_oracle(lanes):
     """C5-shaped run followed by readEventsFile's drain (test_common.go:123-137, on the
@@ -346,6 +422,12 @@ def test_c5_shape_20k_nodes_256_snapshots_vs_oracle_fixture():
         assert got[k] == want[k], k
     sums = g.checksums()
     assert sums["completed"] == fx["snapshots"] and sums["cut_residual"] == 0 and sums["final_residual"] == 0
+    g.poison_outputs()                  # a rerun into poisoned planes reproduces it
+    g.rerun()
+    g.synchronize()
+    got = engine_summary(g)
+    for k in want:
+        assert got[k] == want[k], f"rerun {k}"
 
 
 def test_c5_full_size_properties():

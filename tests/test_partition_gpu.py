@@ -96,3 +96,44 @@ def test_partitioned_device_run_vs_oracle(case):
         np.testing.assert_array_equal(tok, otok)
         np.testing.assert_array_equal(off, ooff)
         np.testing.assert_array_equal(vals, ovals)
+
+
+def _freeze_worker(rank, world, port, out):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import graphcheck as GC
+        p = _program("powerlaw", 2000, 120, 9)
+        g = GC.clg.GraphSim(device=0, fifo_slots=4, max_snapshots=len(p.snap_step))
+        g.set_topology(p.tokens, p.src, p.dst, id_width=p.width())
+        g.set_delay_hash(p.delay_seed)
+        g.set_traffic(p.traffic_seed, p.thresh, p.traffic_steps)
+        ps = GC.clg.PartitionedGraphSim(g, rank, world)
+        ps.run_program(p.steps, p.snap_step, p.snap_rank)
+        out[rank] = (g.status(), ps.frozen, ps.time)
+    except Exception as e:  # surfaced in the parent
+        out[f"error{rank}"] = repr(e)
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_partitioned_freeze_stops_every_rank():
+    """Four FIFO slots per channel overflow at the power-law hubs on one rank (an engine
+    limit, CL_INST_FIFO_OVERFLOW): the status is allgathered with the tick totals, so every
+    rank stops at the same step with the same status instead of drawing from the frozen
+    rank's stale totals -- the whole-graph engine freezes with that status too."""
+    import graphcheck as GC
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_freeze_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    (s0, f0, t0), (s1, f1, t1) = out[0], out[1]
+    assert f0 == f1 != 0 and s0 == s1 == f0 and t0 == t1
+    p = _program("powerlaw", 2000, 120, 9)
+    p.fifo_slots = 4
+    g = GC.engine_program(p)
+    assert g.status() == s0

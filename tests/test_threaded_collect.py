@@ -178,3 +178,64 @@ def test_poll_wait_and_range_collect_over_a_batch():
 def sim_ticks(sim, sid):
     import numpy as np
     return np.array([sim.snapshot_tick(sid, i) for i in range(sim.n_instances)])
+
+
+def test_wait_is_woken_by_ticks_alone():
+    """The reference's driver only calls Tick(); a collector blocked in CollectSnapshot
+    with no timeout must still return (sim.go:137-140): every cl_tick wakes the waiter,
+    whose re-check executes the pending ticks itself."""
+    sc = [s for s in scenarios() if s["name"] == "Test2NodesSingleMessage"][0]
+    sim = cl.ChandyLamportSim(1, seed_base=O.REFERENCE_SEED)
+    sim.read_topology_text(read_text(sc["top"]))
+    lines = [ln for ln in read_text(sc["events"]).split("\n") if ln]
+    out = {}
+
+    def collect():
+        try:
+            out["snap"] = sim.CollectSnapshot(0, 0, timeout_ms=-1)
+        except Exception as e:
+            out["error"] = e
+    th = None
+    for line in lines:
+        f = line.split()
+        if f[0] == "send":
+            sim.ProcessEvent(cl.PassTokenEvent(f[1], f[2], int(f[3])))
+        elif f[0] == "snapshot":
+            sim.StartSnapshot(f[1])
+            th = threading.Thread(target=collect, daemon=True)
+            th.start()
+        else:
+            sim.Tick(int(f[1]) if len(f) > 1 else 1)   # no flush: ticks are only appended
+    for _ in range(200):                                  # the drain, Tick() only
+        if not th.is_alive():
+            break
+        sim.Tick(1)
+        th.join(timeout=0.05)
+    th.join(timeout=30)
+    assert not th.is_alive() and "error" not in out
+    s = out["snap"]
+    assert_equal(read_snapshot_file(sc["snaps"][0]), (s.id, s.tokenMap, [m.astuple() for m in s.messages]))
+
+
+def test_destroy_wakes_blocked_waiter():
+    """cl_sim_destroy wakes a collector blocked in cl_wait_snapshot (it returns
+    CL_E_STATE) and waits for it to leave before freeing the sim."""
+    sim = cl.ChandyLamportSim(4)
+    sim.read_topology_text("2\nA 5\nB 5\nA B\n")       # B -> A missing: the snapshot never completes
+    sim.StartSnapshot("A")
+    sim.flush()
+    out = {}
+
+    def waiter():
+        try:
+            sim.wait_snapshot(0, 0, 4, timeout_ms=-1)
+        except cl.ClSnapError as e:
+            out["code"] = e.code
+    th = threading.Thread(target=waiter, daemon=True)
+    th.start()
+    th.join(timeout=0.5)
+    assert th.is_alive()
+    h, sim._h = sim._h, None
+    assert sim._L.cl_sim_destroy(h) == 0
+    th.join(timeout=10)
+    assert not th.is_alive() and out.get("code") == -8
