@@ -85,6 +85,7 @@ def lib():
         "cl_replay_spill_free": [vp, vp],
         "cl_replay_mapped": [vp, vp],
         "cl_debug_poison_outputs": [vp],
+        "cl_fixup_instances": [vp, vp],
         "cl_num_nodes": [vp, vp],
         "cl_node_id": [vp, i32, vp],
         "cl_num_channels": [vp, vp],
@@ -101,6 +102,8 @@ def lib():
         "cl_poll_snapshot": [vp, i32, i64, i64, vp],
         "cl_wait_snapshot": [vp, i32, i64, i64, i64, vp],
         "cl_collect_snapshot_range": [vp, i32, i64, i64, vp, vp, vp, vp, i64],
+        "cl_collect_snapshot_packed": [vp, i32, i64, i64, vp, vp, vp, vp, i64, vp],
+        "cl_collect_time": [vp, vp],
         "cl_get_counters": [vp, i32, vp],
         "cl_get_checksums": [vp, vp],
         "cl_go_delay_schedule": [i64, i64, i64, vp],
@@ -322,6 +325,33 @@ class ChandyLamportSim:
             _check(rc)
             return tok, done.astype(bool), off, msg[:off[-1]]
 
+    def collect_snapshot_packed(self, snapshot_id, inst_lo=0, inst_hi=None, out=None):
+        """CollectSnapshot of many instances packed on the GPU (cl_collect_snapshot_packed):
+        (tokens int32[n, N], complete bool[n], offsets int64[n * C + 1], messages int32).
+        `out` = (tokens, complete, offsets, messages) arrays to fill (reused across calls; the
+        message array is grown when too small)."""
+        hi = self.n_instances if inst_hi is None else inst_hi
+        k, n, ch = hi - inst_lo, self.num_nodes, self.num_channels
+        if out is None:
+            out = (np.zeros((k, n), dtype=np.int32), np.zeros(k, dtype=np.int32),
+                   np.zeros(k * ch + 1, dtype=np.int64), np.zeros(max(1024, 4 * k), dtype=np.int32))
+        tok, done, off, msg = out
+        m = C.c_int64(0)
+        rc = self._L.cl_collect_snapshot_packed(self._h, snapshot_id, inst_lo, hi, _p(tok), _p(done), _p(off),
+                                                _p(msg), msg.size, C.byref(m))
+        if rc == -7 and m.value > msg.size:
+            msg = np.zeros(m.value, dtype=np.int32)
+            rc = self._L.cl_collect_snapshot_packed(self._h, snapshot_id, inst_lo, hi, _p(tok), _p(done), _p(off),
+                                                    _p(msg), msg.size, C.byref(m))
+        _check(rc)
+        return tok, done.astype(bool), off, msg[:m.value]
+
+    def collect_time(self):
+        """Device ms of the latest packed collect's kernels."""
+        ms = C.c_double(0)
+        _check(self._L.cl_collect_time(self._h, C.byref(ms)))
+        return ms.value
+
     # ---- drivers (test_common.go) -------------------------------------------
     def read_topology_file(self, path):           # test_common.go:29
         _check(self._L.cl_read_topology_file(self._h, path.encode()))
@@ -374,8 +404,15 @@ class ChandyLamportSim:
         _check(self._L.cl_last_kernel_ms(self._h, C.byref(ms)))
         return ms.value
 
+    def fixup_instances(self):
+        """Instances the latest launch's spill fix-up re-ran with HBM spill rings."""
+        v = C.c_int64(0)
+        _check(self._L.cl_fixup_instances(self._h, C.byref(v)))
+        return v.value
+
     def spill_free_replays(self):
-        """True when the next rerun() runs the spill-free kernel (cl_replay_spill_free)."""
+        """True when the next rerun()'s main pass runs the spill-free kernel (the rest
+        goes through the spill fix-up; cl_replay_spill_free)."""
         v = C.c_int32(0)
         _check(self._L.cl_replay_spill_free(self._h, C.byref(v)))
         return bool(v.value)

@@ -38,12 +38,15 @@ constexpr uint32_t kMarkerBit = 0x80000000u;
 constexpr int32_t kMaxTime = 32767 - 8;      // receiveTime <= time + 5 must fit 15 bits
 constexpr int32_t kMaxPayload = 65535;
 
-// ---- per-channel head word (one u32) ---------------------------------------
-//   bits 7..0  : LDS ring head slot
-//   bits 15..8 : queued packets (LDS ring + HBM spill), <= 255
-//   bits 31..16: token packets delivered on the channel so far (recording cursor)
+// ---- per-link column word (one u32, two 16-bit halves accessed separately) ------
+//   lo16 = head word of out-link k (sender side):
+//     bits 7..0  : LDS ring head slot
+//     bits 15..8 : queued packets (LDS ring + HBM spill), <= 255
+//   hi16 = recording cursor of in-link k (receiver side): token packets delivered on the
+//          channel so far
+// Both halves are read and written with 16-bit LDS accesses (ds_read_u16 / ds_write_b16):
+// one column word per link instead of two, with no unpacking.
 constexpr uint32_t kCountOne = 1u << 8;
-constexpr uint32_t kTokDelivOne = 1u << 16;
 constexpr int32_t kMaxQueued = 255;
 constexpr int32_t kMaxChannelTokens = 65535;
 
@@ -114,10 +117,12 @@ struct Layout {
   int32_t ocap_log2;  // HBM spill ring per channel = 1 << ocap_log2 (-1 = none)
   int32_t od, id;     // max out-degree / in-degree over nodes
   int32_t s_cap;      // snapshot ids provisioned
-  int32_t sp;         // u8 pending counters per node: words = ceil(s_cap / 4)
+  int32_t sp;         // u8 counters per node / per instance: words = s_cap / 4 (s_cap % 4 == 0)
   int32_t ipw;        // instances per wave = 64 / N
-  // private column (words)
-  int32_t w_fifo, w_chw, w_cur, w_int, w_pend, w_trig, priv;
+  // private column (words): FIFO rings, link words (out-link head | in-link cursor),
+  // in-link words (degree bounds above kUnrollMaxD), 16-bit trigger entries, u8 pending
+  // counters
+  int32_t w_fifo, w_lnk, w_int, w_pend, w_trig, priv;
   // shared region (words, after the 64 private columns)
   int32_t x_pick, x_tslot, x_off, x_done, x_ndone, x_acc;
   int32_t x_delay_begin;  // words of the shared region zeroed at start (everything before x_delay)
@@ -166,20 +171,19 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
   L.ipw = n_nodes > 0 ? kWave / n_nodes : 0;
   L.wpb = kWavesPerBlock;
   L.w_fifo = 0;
-  L.w_chw = od << cap_log2;
-  L.w_cur = L.w_chw + od;
-  L.w_int = L.w_cur + id;
+  L.w_lnk = od << cap_log2;
+  L.w_int = L.w_lnk + (od > id ? od : id);
   // in-link words live in registers when the kernel's degree bound is unrolled
   L.w_trig = L.w_int + (unr ? 0 : id);
-  L.w_pend = L.w_trig + id;
+  L.w_pend = L.w_trig + (id + 1) / 2;  // 16-bit trigger entries, at most id per tick
   L.priv = L.w_pend + L.sp;
   // shared region first (its fixed-size arrays at compile-time offsets 0, 64, 128, 192),
   // then the 64 private columns from word `col`
   L.x_pick = 0;
   L.x_tslot = kWave;
   L.x_off = 2 * kWave;
-  L.x_done = 3 * kWave;
-  L.x_ndone = L.x_done + L.ipw * s_cap;
+  L.x_done = 3 * kWave;                      // u8 completion counters per (instance, snapshot)
+  L.x_ndone = L.x_done + L.ipw * L.sp;
   L.x_acc = L.x_ndone + L.ipw;
   L.x_delay_begin = L.x_acc + 5 * L.ipw;
   const int64_t delay_words = (int64_t)L.ipw * sched_row / 4;  // sched_row is a multiple of 16
@@ -201,8 +205,8 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
 // (make_layout with od = id = D): compile-time offsets.
 template <int D, int CAP>
 struct ColumnC {
-  static constexpr int32_t w_fifo = 0, w_chw = D << CAP, w_cur = w_chw + D, w_int = w_cur + D, w_trig = w_int,
-                           w_pend = w_trig + D;
+  static constexpr int32_t w_fifo = 0, w_lnk = D << CAP, w_int = w_lnk + D, w_trig = w_int,
+                           w_pend = w_trig + (D + 1) / 2;
 };
 
 // Kernel parameters (passed by value).
@@ -229,8 +233,15 @@ struct ExecParams {
   int32_t* snap_tick;  // [stride][S_cap]      completion tick or -1 (one row per instance)
   uint32_t* ovf;       // [C][1 << ocap_log2] spill ring
   uint32_t* ovh;       // [C] spill ring head
-  uint32_t* spilled;   // set to 1 by any push that went to a spill ring (cl_host: spill-free replays)
-  int32_t nospill;     // this replay is known to fit the LDS rings: run the spill-free kernel
+  // Spill fix-up (fresh full runs whose layout has spill rings; cl_kernels.hip launch_exec):
+  // the main pass runs the spill-free kernel and appends every instance it froze with
+  // FIFO_OVERFLOW to fix_list; a second launch re-runs exactly those instances from the
+  // initial state with the spill-capable kernel, and zeroes fix_clear (the counter the next
+  // main pass appends to).  nullptr: no fix-up (resumed launches, trace runs).
+  uint32_t* fix_list;  // [n_inst] instances to re-run
+  uint32_t* fix_count; // entries of fix_list
+  uint32_t* fix_clear; // the other counter of the pair
+  int32_t fix_blocks;  // fix-up grid (persistent waves over the list)
   // slot -> instance for a replay (nullptr: slot i runs instance i).  cl_host orders a
   // replay's instances by their final tick so the segments of a wave finish together
   const int32_t* inst_map;
@@ -269,9 +280,38 @@ struct ExecLaunch {
   void* stream;
   void* ev_start;
   void* ev_stop;
+  int32_t* fixup_launched;  // out: 1 when a spill fix-up launch followed the main pass
 };
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
 int launch_checksums(const SumParams& p, void* stream);
+
+// CollectSnapshot (sim.go:134-173) of snapshot `sid` for instances [lo, lo + n), packed on
+// the device (cl_kernels.hip): the node records' token words and the recording cursors are
+// expanded over the channels' token histories into one CSR over (instance, channel), channels
+// in (src rank, dest rank) order, messages in delivery order (finalizeSnapshot node.go:188-195
+// per channel).  Only the packed arrays cross PCIe.
+struct PackParams {
+  int32_t n_nodes, n_ch, s_cap, rw, sid;
+  int64_t lo, n, stride;
+  const uint32_t* snap_nod;
+  const int32_t* snap_tick;
+  const int32_t* ch_slot;
+  const int32_t* hist_off;  // [C + 1]
+  const int32_t* hist_val;
+  int32_t* tokens;          // [n][N] tokenMap by rank, -1 where the snapshot has not completed
+  int32_t* complete;        // [n]
+  long long* count;         // [n + 1] messages per instance -> exclusive prefix (count[n] = total)
+  long long* bsum;          // scan scratch: one per block of kScanItems instances
+  long long* offsets;       // [n * C + 1]
+  int32_t* msgs;            // [total]
+};
+constexpr int32_t kScanItems = 2048;  // instances per scan block (256 threads x 8)
+// count + scan (total left in p.count[n]), then fill: two calls so the host can size msgs.
+int launch_pack_count(const PackParams& p, void* stream);
+int launch_pack_fill(const PackParams& p, void* stream);
+// Recorded message copies (node.go:179-183) over every instance's completed snapshots:
+// out[0] all instances, out[1] status-OK instances.
+int launch_recorded(const SumParams& p, void* stream);
 
 // Snapshot content hash (shared definition with oracle/cl_oracle.c orc_snapshot_hash).
 #if defined(__HIPCC__)

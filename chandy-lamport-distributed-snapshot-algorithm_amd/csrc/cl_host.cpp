@@ -49,8 +49,10 @@ const char* last_error() { return g_last_error.c_str(); }
 // Per-wave LDS words available for staging the wave's delay rows (kernel reads the
 // delays from LDS instead of HBM when ipw * row fits).
 constexpr int32_t kDelayStageWords = 2048;
-// Workgroups (4 waves each) per CU the automatic FIFO sizing keeps LDS from limiting.
-constexpr int32_t kTargetBlocks = 4;
+// Workgroups (4 waves each) per CU the automatic FIFO sizing keeps LDS from limiting (the
+// spill-free kernels of degree bounds 3-4 run 6 waves per SIMD; deeper queues go through the
+// spill fix-up).
+constexpr int32_t kTargetBlocks = 6;
 // Batches of at least this many instances replay through a length-ordered slot map (a few
 // thousand waves: the grouping pays for its one host sort and 4 B per instance of HBM).
 constexpr int64_t kMapMinInstances = 4096;
@@ -275,14 +277,13 @@ struct cl_sim {
   DevBuf<int32_t> d_snap_tick;
   DevBuf<uint32_t> d_ovf;
   DevBuf<uint32_t> d_ovh;
-  DevBuf<uint32_t> d_spilled;  // 1 word: a push of the last spill-capable launch used a spill ring
-  // A fresh full run of ops [0, nospill_ops) with these delays and layout spilled nothing: its
-  // replays (cl_rerun: the same program and delays, hence the same queues) run the
-  // spill-free kernel.  -1: unknown.
-  int64_t nospill_ops = -1;
-  int64_t spill_tried = -1;    // the program length the last probe ran for (no probe twice)
-  bool spill_probe = false;    // the last launch was a fresh spill-capable full run (of probe_ops ops)
-  int64_t probe_ops = 0;
+  // Spill fix-up of fresh full runs (cl_kernels.hip launch_exec_fixup): the spill-free main
+  // pass lists the instances its LDS rings could not hold; the fix-up re-runs them with the
+  // HBM spill rings.  Two worklist counters alternate: a pair's fix-up zeroes the other one.
+  DevBuf<uint32_t> d_fix;      // [n_inst] worklist
+  DevBuf<uint32_t> d_fixc;     // [2] counters
+  int32_t fix_par = 0;         // counter the next main pass appends to
+  int32_t fix_last = -1;       // counter the last fix-up pair used (-1: none)
   // Replays grouped by length: after a fresh full run of ops [0, map_ops) the host orders the
   // instances by their final tick (d_map: slot -> instance) so the 64 / N instances sharing a
   // wave end their drains together; replays of the same program and delays launch through
@@ -301,10 +302,18 @@ struct cl_sim {
   int64_t trace_lo = 0;
   int32_t trace_n = 0, trace_cap = 0;
 
-  // host mirrors of results (invalidated by every launch)
+  // host mirrors of the per-instance results (invalidated by every launch); the snapshot
+  // records stay on the device: collects pack them there (cl_pack_*), a one-instance collect
+  // copies that instance's records only
   bool h_valid = false;
   std::vector<int32_t> h_regs, h_snap_tick, h_tok, ch_slot;
-  std::vector<uint32_t> h_snap_nod;
+  // device-side CollectSnapshot packing (PackParams)
+  DevBuf<int32_t> d_pk_tok, d_pk_done, d_pk_msg;
+  DevBuf<long long> d_pk_cnt, d_pk_bsum, d_pk_off;
+  DevBuf<unsigned long long> d_rec2;
+  hipEvent_t pk_ev[2] = {nullptr, nullptr};
+  bool pk_timed = false;
+  size_t hist_uploaded = (size_t)-1;  // history entries on the device
 
   ~cl_sim() {
     if (dev_ready) {
@@ -312,8 +321,12 @@ struct cl_sim {
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
-      d_ovh.release(); d_spilled.release(); d_map.release(); d_hist.release(); d_sums.release();
+      d_ovh.release(); d_fix.release(); d_fixc.release(); d_map.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
+      d_pk_tok.release(); d_pk_done.release(); d_pk_msg.release(); d_pk_cnt.release(); d_pk_bsum.release();
+      d_pk_off.release(); d_rec2.release();
+      for (auto& e : pk_ev)
+        if (e) (void)hipEventDestroy(e);
       for (auto& e : ev_pool) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -446,7 +459,6 @@ struct cl_sim {
       if (rc) return rc;
       HIP_TRY(hipMemcpy(d_sched.p, sched.data(), sched.size(), hipMemcpyHostToDevice));
       dev_draws = D;  // longer rows of the same streams: saved draw cursors stay valid
-      nospill_ops = spill_tried = -1;
       map_ops = map_tried = -1;
       dev_row = D;
       return CL_OK;
@@ -462,7 +474,6 @@ struct cl_sim {
     HIP_TRY(hipMemcpy(d_sched.p, padded.data(), padded.size(), hipMemcpyHostToDevice));
     dev_draws = user_draws;
     dev_row = row;
-    nospill_ops = spill_tried = -1;
     map_ops = map_tried = -1;
     return CL_OK;
   }
@@ -520,14 +531,25 @@ struct cl_sim {
     const size_t ov = lay.ocap_log2 >= 0 ? ((size_t)C << lay.ocap_log2) * stride : 1;
     if ((rc = d_ovf.ensure(ov))) return rc;
     if ((rc = d_ovh.ensure(lay.ocap_log2 >= 0 ? (size_t)std::max(C, 1) * stride : 1))) return rc;
-    if ((rc = d_spilled.ensure(1))) return rc;
-    nospill_ops = spill_tried = -1;  // (a new layout: probe again)
+    if (lay.ocap_log2 >= 0) {
+      if ((rc = d_fix.ensure((size_t)n_inst))) return rc;
+      if (!d_fixc.p) {
+        if ((rc = d_fixc.ensure(2))) return rc;
+        HIP_TRY(hipMemset(d_fixc.p, 0, 2 * sizeof(uint32_t)));
+        fix_par = 0;
+        fix_last = -1;
+      }
+    }
     map_ops = map_tried = -1;
     need_fresh = true;
     return CL_OK;
   }
 
   int upload_hist() {
+    size_t tot = 0;
+    for (auto& h : hist) tot += h.size();
+    if (tot == hist_uploaded && d_hist.p) return CL_OK;  // (histories only grow: same size, same data)
+    hist_uploaded = tot;
     std::vector<int32_t> off(1, 0), val;
     for (auto& h : hist) {
       val.insert(val.end(), h.begin(), h.end());
@@ -593,7 +615,6 @@ struct cl_sim {
     p.snap_tick = d_snap_tick.p;
     p.ovf = d_ovf.p;
     p.ovh = d_ovh.p;
-    p.spilled = d_spilled.p;
     p.ch_dest = d_ch_dest.p;
     if (trace_n > 0) {
       p.trace = d_trace.p;
@@ -641,19 +662,17 @@ struct cl_sim {
     // cl_exec_kernel prologue -- no fill launch before every replay)
     ExecParams p = exec_params(begin, started_before);
     p.save_state = save_state ? 1 : 0;
-    // spill-free replays: a fresh full run whose program and delays already ran once without
-    // touching a spill ring (the same replay fills the same queues)
-    p.nospill = begin == 0 && trace_n == 0 && nospill_ops == (int64_t)ops.size() ? 1 : 0;
+    // a fresh full run with spill rings in the layout: spill-free main pass + fix-up (the
+    // launcher decides whether its kernels are specialized for the layout)
+    if (begin == 0 && trace_n == 0 && lay.ocap_log2 >= 0) {
+      p.fix_list = d_fix.p;
+      p.fix_count = d_fixc.p + fix_par;
+      p.fix_clear = d_fixc.p + (fix_par ^ 1);
+      p.fix_blocks = fix_blocks();
+    }
     p.inst_map = begin == 0 && map_ops == (int64_t)ops.size() ? d_map.p : nullptr;
     map_probe = begin == 0 && !p.inst_map && n_inst >= kMapMinInstances && map_tried != (int64_t)ops.size();
     map_probe_ops = (int64_t)ops.size();
-    // (a probe clears a device flag with a copy on the stream: once per program, not per
-    // replay -- per replay it put a ~10 us gap between the benchmark's launches)
-    spill_probe = begin == 0 && trace_n == 0 && !p.nospill && lay.ocap_log2 >= 0 && spill_tried != (int64_t)ops.size();
-    if (spill_probe) {
-      probe_ops = (int64_t)ops.size();
-      HIP_TRY(hipMemsetAsync(d_spilled.p, 0, sizeof(uint32_t), stream));
-    }
     if (ev_used == 256 && (rc = fold_events())) return rc;
     if (ev_used == ev_pool.size()) {
       std::pair<hipEvent_t, hipEvent_t> pr;
@@ -665,8 +684,15 @@ struct cl_sim {
     // the dispatch records both events (the kernel's own start/end timestamps): two
     // hipEventRecord packets around it cost 0.7 us more per launch (C2 0.1816 -> 0.1809 ms per
     // step) and bracketed ~1 us of packet processing into the kernel time
-    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p, ExecLaunch{stream, pr.first, pr.second});
+    int32_t fixed = 0;
+    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p, ExecLaunch{stream, pr.first, pr.second, &fixed});
     if (e != 0) return set_err(CL_E_DEVICE, "exec kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    if (fixed) {  // this pair used counter fix_par and zeroed the other for the next pair
+      fix_last = fix_par;
+      fix_par ^= 1;
+    } else {
+      fix_last = -1;
+    }
     ev0 = pr.first;
     ev1 = pr.second;
     timed = true;
@@ -677,17 +703,28 @@ struct cl_sim {
     return CL_OK;
   }
 
+  // The launcher's specialized kernels (and so the spill fix-up) serve this layout: unrolled
+  // degree bound, staged delays, 2 / 4 / 8 LDS ring slots (cl_kernels.hip launch_exec_d).
+  bool specialized() const {
+    const int32_t d = std::max(std::max(max_out, max_in), 1);
+    return degree_bound(d) <= kUnrollMaxD && lay.x_delay > 0 && lay.cap_log2 >= 1 && lay.cap_log2 <= 3;
+  }
+
+  // Fix-up grid: persistent waves over the worklist, sized to the resident capacity of the
+  // fix-up kernel (3 waves per SIMD: it keeps its registers; LDS per CU)
+  int32_t fix_blocks() const {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    const int64_t by_lds = (int64_t)kMaxLdsBytes / std::max<int64_t>(1, (int64_t)lay.wave_words * 4 * lay.wpb);
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(3, by_lds));
+    const int64_t need = ((n_inst + lay.ipw - 1) / lay.ipw + lay.wpb - 1) / lay.wpb;
+    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(need, per_cu * cus));
+  }
+
   int sync() {
     if (!dev_ready) return CL_OK;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamSynchronize(stream));
-    if (spill_probe) {
-      uint32_t sp = 1;
-      HIP_TRY(hipMemcpy(&sp, d_spilled.p, sizeof sp, hipMemcpyDeviceToHost));
-      if (!sp) nospill_ops = probe_ops;
-      spill_tried = probe_ops;
-      spill_probe = false;
-    }
     if (map_probe) {
       map_probe = false;
       int rc = build_map();
@@ -785,26 +822,96 @@ struct cl_sim {
     if (!dev_ready) return set_err(CL_E_STATE, "nothing has run on the device yet");
     const int n = (int)ids.size();
     h_regs.resize((size_t)R_NUM * stride);
-    h_snap_nod.resize((size_t)s_cap * n * lay.rw * stride);
     h_snap_tick.resize((size_t)s_cap * stride);
     h_tok.resize((size_t)n * stride);
     HIP_TRY(hipMemcpy(h_regs.data(), d_regs.p, h_regs.size() * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(h_snap_nod.data(), d_snap_nod.p, h_snap_nod.size() * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(h_snap_tick.data(), d_snap_tick.p, h_snap_tick.size() * 4, hipMemcpyDeviceToHost));
     if (n) HIP_TRY(hipMemcpy(h_tok.data(), d_fin_tok.p, h_tok.size() * 4, hipMemcpyDeviceToHost));
     h_valid = true;
     return CL_OK;
   }
 
-  // Host copies of the node snapshot records (after fetch): tokenMap entry of node v and the
-  // cursor word of channel c in snapshot sid of instance inst.
-  const uint32_t* rec_base(int sid, int64_t inst) const {
-    return &h_snap_nod[((size_t)sid * stride + inst) * ids.size() * lay.rw];
-  }
   int32_t reg(int64_t inst, int r) const { return h_regs[(size_t)inst * R_NUM + r]; }
   int32_t tick_at(int sid, int64_t inst) const { return h_snap_tick[(size_t)inst * s_cap + sid]; }
-  int32_t tok_at(int sid, int64_t inst, int v) const { return (int32_t)rec_base(sid, inst)[(size_t)v * lay.rw]; }
-  uint32_t rec_at(int sid, int64_t inst, int c) const { return rec_base(sid, inst)[ch_slot[c]]; }
+  // The node snapshot records of one (snapshot, instance): N * rw words (tokenMap entry of
+  // node v at v * rw, the cursor word of channel c at ch_slot[c]).
+  int records(int sid, int64_t inst, std::vector<uint32_t>* out) const {
+    const size_t w = ids.size() * (size_t)lay.rw;
+    out->resize(w);
+    HIP_TRY(hipMemcpy(out->data(), d_snap_nod.p + ((size_t)sid * stride + inst) * w, w * 4, hipMemcpyDeviceToHost));
+    return CL_OK;
+  }
+
+  SumParams sum_params() const {
+    SumParams p{};
+    p.n_nodes = (int32_t)ids.size();
+    p.n_ch = (int32_t)ch_dst.size();
+    p.s_cap = s_cap;
+    p.n_sids = n_sids;
+    p.n_inst = n_inst;
+    p.stride = stride;
+    p.regs = d_regs.p;
+    p.rw = lay.rw;
+    p.snap_nod = d_snap_nod.p;
+    p.ch_slot = d_ch_slot.p;
+    p.snap_tick = d_snap_tick.p;
+    p.fin_tok = d_fin_tok.p;
+    p.hist_off = d_hist.p;
+    p.hist_val = d_hist.p + hist.size() + 1;
+    p.total_tokens = total_tokens;
+    return p;
+  }
+
+  // CollectSnapshot of instances [lo, hi) packed on the device (cl_pack_count / cl_pack_fill):
+  // the packed arrays stay in d_pk_*; *total = messages.  Times the kernels (cl_collect_time).
+  int pack(int32_t sid, int64_t lo, int64_t hi, int64_t* total) {
+    int rc = flush();
+    if (rc) return rc;
+    if (!dev_ready) return set_err(CL_E_STATE, "nothing has run on the device yet");
+    HIP_TRY(hipSetDevice(device));
+    if ((rc = upload_hist())) return rc;
+    const int64_t n = hi - lo;
+    const int N = (int)ids.size(), C = (int)ch_dst.size();
+    if ((rc = d_pk_tok.ensure((size_t)std::max<int64_t>(n, 1) * N)) || (rc = d_pk_done.ensure((size_t)n + 1)) ||
+        (rc = d_pk_cnt.ensure((size_t)n + 1)) || (rc = d_pk_bsum.ensure((size_t)(n / kScanItems + 1))) ||
+        (rc = d_pk_off.ensure((size_t)n * C + 1)))
+      return rc;
+    for (auto& e : pk_ev)
+      if (!e) HIP_TRY(hipEventCreate(&e));
+    PackParams p{};
+    p.n_nodes = N;
+    p.n_ch = C;
+    p.s_cap = s_cap;
+    p.rw = lay.rw;
+    p.sid = sid;
+    p.lo = lo;
+    p.n = n;
+    p.stride = stride;
+    p.snap_nod = d_snap_nod.p;
+    p.snap_tick = d_snap_tick.p;
+    p.ch_slot = d_ch_slot.p;
+    p.hist_off = d_hist.p;
+    p.hist_val = d_hist.p + hist.size() + 1;
+    p.tokens = d_pk_tok.p;
+    p.complete = d_pk_done.p;
+    p.count = d_pk_cnt.p;
+    p.bsum = d_pk_bsum.p;
+    p.offsets = d_pk_off.p;
+    HIP_TRY(hipEventRecord(pk_ev[0], stream));
+    int e = launch_pack_count(p, stream);
+    if (e) return set_err(CL_E_DEVICE, "pack kernels: %s", hipGetErrorString((hipError_t)e));
+    long long tot = 0;
+    HIP_TRY(hipMemcpyAsync(&tot, d_pk_cnt.p + n, sizeof tot, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if ((rc = d_pk_msg.ensure((size_t)std::max<long long>(tot, 1)))) return rc;
+    p.msgs = d_pk_msg.p;
+    e = launch_pack_fill(p, stream);
+    if (e) return set_err(CL_E_DEVICE, "pack kernels: %s", hipGetErrorString((hipError_t)e));
+    HIP_TRY(hipEventRecord(pk_ev[1], stream));
+    pk_timed = true;
+    *total = tot;
+    return CL_OK;
+  }
 
   int append(Op op) {
     int rc = freeze();
@@ -949,7 +1056,6 @@ int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks) 
 
 int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
   SIM_CHECK(sim);
-  sim->nospill_ops = sim->spill_tried = -1;
   sim->map_ops = sim->map_tried = -1;
   sim->go_seeds = true;
   sim->seed_base = seed_base;
@@ -960,7 +1066,6 @@ int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
 
 int cl_set_delay_schedule(cl_sim* sim, const uint8_t* delays, int64_t draws_per_instance) {
   SIM_CHECK(sim);
-  sim->nospill_ops = sim->spill_tried = -1;
   sim->map_ops = sim->map_tried = -1;
   if (!delays || draws_per_instance <= 0) return set_err(CL_E_INVALID, "empty schedule");
   const size_t n = (size_t)(draws_per_instance * sim->n_inst);
@@ -1091,9 +1196,22 @@ int cl_rerun(cl_sim* sim) {
 int cl_replay_spill_free(cl_sim* sim, int32_t* on) {
   SIM_CHECK(sim);
   if (!on) return set_err(CL_E_INVALID, "null output");
-  int rc = sim->sync();  // (a pending spill probe is read here)
+  int rc = sim->sync();
   if (rc) return rc;
-  *on = sim->lay.ocap_log2 < 0 || sim->nospill_ops == (int64_t)sim->ops.size() ? 1 : 0;
+  *on = sim->lay.ocap_log2 < 0 || sim->specialized() ? 1 : 0;
+  return CL_OK;
+}
+
+int cl_fixup_instances(cl_sim* sim, int64_t* n) {
+  SIM_CHECK(sim);
+  if (!n) return set_err(CL_E_INVALID, "null output");
+  int rc = sim->sync();
+  if (rc) return rc;
+  *n = 0;
+  if (sim->fix_last < 0) return CL_OK;
+  uint32_t c = 0;  // (zeroed only by the next pair's fix-up)
+  HIP_TRY(hipMemcpy(&c, sim->d_fixc.p + sim->fix_last, sizeof c, hipMemcpyDeviceToHost));
+  *n = c;
   return CL_OK;
 }
 
@@ -1259,12 +1377,14 @@ int cl_collect_snapshot(cl_sim* sim, int32_t sid, int64_t inst, int64_t* tokens,
   if (sim->tick_at(sid, inst) < 0)
     return set_err(CL_E_NOT_COMPLETE, "snapshot %d has not completed in instance %lld", sid, (long long)inst);
   const int n = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
-  for (int v = 0; v < n; ++v) tokens[v] = sim->tok_at(sid, inst, v);
+  std::vector<uint32_t> rb;
+  if ((rc = sim->records(sid, inst, &rb))) return rc;
+  for (int v = 0; v < n; ++v) tokens[v] = (int32_t)rb[(size_t)v * sim->lay.rw];
   int64_t m = 0;
   bool fits = true;
   for (int c = 0; c < C; ++c) {
     msg_offsets[c] = m;
-    const uint32_t rec = sim->rec_at(sid, inst, c);
+    const uint32_t rec = rb[sim->ch_slot[c]];
     const uint32_t b = rec & 0xffffu, e = rec >> 16;
     for (uint32_t k = b; k < e; ++k, ++m) {
       if (m < msg_cap) msg_tokens[m] = sim->hist[c][k];
@@ -1323,30 +1443,58 @@ int cl_collect_snapshot_range(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t
   SIM_CHECK(sim);
   if (sid < 0 || sid >= sim->n_sids || inst_lo < 0 || inst_hi > sim->n_inst || inst_lo > inst_hi)
     return set_err(CL_E_INVALID, "snapshot/instance range out of range");
-  int rc = sim->fetch();
+  int64_t tot = 0;
+  int rc = sim->pack(sid, inst_lo, inst_hi, &tot);
   if (rc) return rc;
-  const int n = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
-  int64_t m = 0;
-  bool fits = true;
-  for (int64_t i = inst_lo; i < inst_hi; ++i) {
-    const int64_t r = i - inst_lo;
-    const bool done = sim->tick_at(sid, i) >= 0;
-    if (complete) complete[r] = done ? 1 : 0;
-    if (tokens)
-      for (int v = 0; v < n; ++v) tokens[r * n + v] = done ? sim->tok_at(sid, i, v) : -1;
-    for (int c = 0; c < C; ++c) {
-      if (msg_offsets) msg_offsets[r * C + c] = m;
-      if (!done) continue;
-      const uint32_t rec = sim->rec_at(sid, i, c);
-      const uint32_t b = rec & 0xffffu, e = rec >> 16;
-      for (uint32_t k = b; k < e; ++k, ++m) {
-        if (m < msg_cap && msg_tokens) msg_tokens[m] = sim->hist[c][k];
-        else fits = false;
-      }
-    }
+  const int64_t n = inst_hi - inst_lo;
+  const int N = (int)sim->ids.size(), C = (int)sim->ch_dst.size();
+  if (complete) HIP_TRY(hipMemcpy(complete, sim->d_pk_done.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  if (msg_offsets) HIP_TRY(hipMemcpy(msg_offsets, sim->d_pk_off.p, ((size_t)n * C + 1) * 8, hipMemcpyDeviceToHost));
+  if (tokens) {  // (the int64 ABI widens on the host)
+    std::vector<int32_t> t((size_t)n * N);
+    if (!t.empty()) HIP_TRY(hipMemcpy(t.data(), sim->d_pk_tok.p, t.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < t.size(); ++k) tokens[k] = t[k];
   }
-  if (msg_offsets) msg_offsets[(inst_hi - inst_lo) * C] = m;
-  return fits ? CL_OK : set_err(CL_E_LIMIT, "msg_cap %lld < %lld messages", (long long)msg_cap, (long long)m);
+  if (tot > msg_cap || (tot > 0 && !msg_tokens))
+    return set_err(CL_E_LIMIT, "msg_cap %lld < %lld messages", (long long)msg_cap, (long long)tot);
+  if (tot > 0) {
+    std::vector<int32_t> m((size_t)tot);
+    HIP_TRY(hipMemcpy(m.data(), sim->d_pk_msg.p, m.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < m.size(); ++k) msg_tokens[k] = m[k];
+  }
+  return CL_OK;
+}
+
+int cl_collect_snapshot_packed(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int32_t* tokens,
+                               int32_t* complete, int64_t* msg_offsets, int32_t* msg_tokens, int64_t msg_cap,
+                               int64_t* n_msgs) {
+  SIM_CHECK(sim);
+  if (sid < 0 || sid >= sim->n_sids || inst_lo < 0 || inst_hi > sim->n_inst || inst_lo > inst_hi)
+    return set_err(CL_E_INVALID, "snapshot/instance range out of range");
+  int64_t tot = 0;
+  int rc = sim->pack(sid, inst_lo, inst_hi, &tot);
+  if (rc) return rc;
+  if (n_msgs) *n_msgs = tot;
+  const size_t n = (size_t)(inst_hi - inst_lo), N = sim->ids.size(), C = sim->ch_dst.size();
+  if (tokens && n) HIP_TRY(hipMemcpyAsync(tokens, sim->d_pk_tok.p, n * N * 4, hipMemcpyDeviceToHost, sim->stream));
+  if (complete && n) HIP_TRY(hipMemcpyAsync(complete, sim->d_pk_done.p, n * 4, hipMemcpyDeviceToHost, sim->stream));
+  if (msg_offsets) HIP_TRY(hipMemcpyAsync(msg_offsets, sim->d_pk_off.p, (n * C + 1) * 8, hipMemcpyDeviceToHost, sim->stream));
+  const bool fits = tot <= msg_cap && (tot == 0 || msg_tokens);
+  if (fits && tot > 0)
+    HIP_TRY(hipMemcpyAsync(msg_tokens, sim->d_pk_msg.p, (size_t)tot * 4, hipMemcpyDeviceToHost, sim->stream));
+  HIP_TRY(hipStreamSynchronize(sim->stream));
+  return fits ? CL_OK : set_err(CL_E_LIMIT, "msg_cap %lld < %lld messages", (long long)msg_cap, (long long)tot);
+}
+
+int cl_collect_time(cl_sim* sim, double* device_ms) {
+  SIM_CHECK(sim);
+  if (!device_ms) return set_err(CL_E_INVALID, "null output");
+  if (!sim->pk_timed) return set_err(CL_E_STATE, "no packed collect has run");
+  HIP_TRY(hipStreamSynchronize(sim->stream));
+  float f = 0.f;
+  HIP_TRY(hipEventElapsedTime(&f, sim->pk_ev[0], sim->pk_ev[1]));
+  *device_ms = f;
+  return CL_OK;
 }
 
 int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out) {
@@ -1354,8 +1502,6 @@ int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out) {
   int rc = sim->fetch();
   if (rc) return rc;
   for (int k = 0; k < CL_NUM_COUNTERS; ++k) out[k] = 0;
-  const int C = (int)sim->ch_dst.size();
-
   for (int64_t i = 0; i < sim->n_inst; ++i) {
     if (only_ok && sim->reg(i, R_STATUS) != ST_OK) continue;
     out[CL_CNT_PUSH] += (uint32_t)sim->reg(i, R_PUSH);
@@ -1365,14 +1511,19 @@ int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out) {
     out[CL_CNT_COMPLETED] += sim->reg(i, R_NDONE);
     out[CL_CNT_INSTANCES] += 1;
     out[CL_CNT_TICKS] += sim->reg(i, R_TIME);
-    for (int32_t s = 0; s < sim->n_sids; ++s) {
-      if (sim->tick_at(s, i) < 0) continue;
-      for (int c = 0; c < C; ++c) {
-        const uint32_t rec = sim->rec_at(s, i, c);
-        out[CL_CNT_RECORDED] += (rec >> 16) - (rec & 0xffffu);
-      }
-    }
   }
+  // recorded copies over completed snapshots: summed on the device from the node records
+  HIP_TRY(hipSetDevice(sim->device));
+  if ((rc = sim->d_rec2.ensure(2))) return rc;
+  HIP_TRY(hipMemsetAsync(sim->d_rec2.p, 0, 2 * sizeof(unsigned long long), sim->stream));
+  SumParams p = sim->sum_params();
+  p.out = sim->d_rec2.p;
+  int e = launch_recorded(p, sim->stream);
+  if (e) return set_err(CL_E_DEVICE, "recorded-count kernel: %s", hipGetErrorString((hipError_t)e));
+  unsigned long long r[2];
+  HIP_TRY(hipMemcpyAsync(r, sim->d_rec2.p, sizeof r, hipMemcpyDeviceToHost, sim->stream));
+  HIP_TRY(hipStreamSynchronize(sim->stream));
+  out[CL_CNT_RECORDED] = (int64_t)r[only_ok ? 1 : 0];
   return CL_OK;
 }
 
@@ -1385,22 +1536,7 @@ int cl_get_checksums(cl_sim* sim, int64_t* out) {
   if ((rc = sim->upload_hist())) return rc;
   if ((rc = sim->d_sums.ensure(CL_NUM_SUMS))) return rc;
   HIP_TRY(hipMemsetAsync(sim->d_sums.p, 0, CL_NUM_SUMS * sizeof(unsigned long long), sim->stream));
-  SumParams p{};
-  p.n_nodes = (int32_t)sim->ids.size();
-  p.n_ch = (int32_t)sim->ch_dst.size();
-  p.s_cap = sim->s_cap;
-  p.n_sids = sim->n_sids;
-  p.n_inst = sim->n_inst;
-  p.stride = sim->stride;
-  p.regs = sim->d_regs.p;
-  p.rw = sim->lay.rw;
-  p.snap_nod = sim->d_snap_nod.p;
-  p.ch_slot = sim->d_ch_slot.p;
-  p.snap_tick = sim->d_snap_tick.p;
-  p.fin_tok = sim->d_fin_tok.p;
-  p.hist_off = sim->d_hist.p;
-  p.hist_val = sim->d_hist.p + sim->hist.size() + 1;
-  p.total_tokens = sim->total_tokens;
+  SumParams p = sim->sum_params();
   p.out = sim->d_sums.p;
   int e = launch_checksums(p, sim->stream);
   if (e) return set_err(CL_E_DEVICE, "checksum kernel launch failed: %s", hipGetErrorString((hipError_t)e));

@@ -51,6 +51,7 @@ namespace {
 // merge an LDS store with a global one into a FLAT store, and every FLAT op forces
 // s_waitcnt vmcnt(0) lgkmcnt(0) -- a full memory drain inside the tick loop.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 // Uniform-per-lane context.  Output arrays are addressed with 32-bit element indices
@@ -157,6 +158,13 @@ using InLinks = uint32_t[unrolled(D) ? D : 1];
 
 #define PW(k) (x.P[(uint32_t)(k) << 6])
 #define XW(k) (x.X[(uint32_t)(k)])
+// 16-bit half h of this lane's column word k: link word halves and trigger entries
+#define PH(k, h) (reinterpret_cast<lds_u16*>(x.P + ((uint32_t)(k) << 6))[h])
+// out-link ko's head word (lo16) and in-link ki's recording cursor (hi16) of link word k
+#define CHW(ko) PH(lay.w_lnk + (ko), 0)
+#define CUR(ki) PH(lay.w_lnk + (ki), 1)
+// trigger entry k (16 bit: sender rank | snapshot id << 8)
+#define TRIG(k) PH(lay.w_trig + ((uint32_t)(k) >> 1), (k) & 1)
 
 // LDS atomic add (ds_add_rtn_u32); the wave's lanes are the only users of these words.
 __device__ __forceinline__ uint32_t lds_add(lds_u32* a, uint32_t v) {
@@ -189,8 +197,8 @@ template <bool STAGED>
 __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int64_t k) {
   const Layout& lay = x.lay;
   if (k >= x.p.draws) { ln.flag = ST_DELAY_EXHAUSTED; return; }
-  const uint32_t chw = PW(lay.w_chw + ko);
-  const uint32_t cnt = (chw >> 8) & 0xffu;
+  const uint32_t chw = CHW(ko);
+  const uint32_t cnt = chw >> 8;
   if (cnt >= (uint32_t)kMaxQueued) { ln.flag = ST_FIFO_OVERFLOW; return; }
   uint32_t delay;
   if constexpr (STAGED) delay = x.lrow[k];
@@ -210,9 +218,8 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
     if (cnt == cap) *hp = 0u;
     else h = *hp;
     x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.stride + x.inst] = e;
-    *x.p.spilled = 1u;  // (a replay of this program needs the spill rings)
   }
-  PW(lay.w_chw + ko) = chw + kCountOne;
+  CHW(ko) = (uint16_t)(chw + kCountOne);
   ln.push++;
 }
 
@@ -232,7 +239,7 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
     r[0] = (uint32_t)ln.tokens;
 #pragma unroll
     for (int32_t kj = 0; kj < RW - 1; ++kj) {
-      const uint32_t cur = (kj < D && kj < x.indeg) ? PW(lay.w_cur + kj) : 0u;
+      const uint32_t cur = (kj < D && kj < x.indeg) ? (uint32_t)CUR(kj) : 0u;
       r[1 + kj] = kj == arrive ? (cur | (cur << 16)) : cur;
     }
     (void)it;
@@ -246,7 +253,7 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
   } else {
     st_snap(p.snap_nod, rb, (uint32_t)ln.tokens);
     for (int32_t kj = 0; kj < x.indeg; ++kj) {
-      const uint32_t cur = PW(lay.w_cur + kj);
+      const uint32_t cur = CUR(kj);
       st_snap(p.snap_nod, rb + 4u * (1 + kj), kj == arrive ? (cur | (cur << 16)) : cur);
     }
   }
@@ -254,9 +261,11 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
 
 // NotifyCompletedSnapshot (sim.go:126-131): the instance's snapshot completes when all N
 // nodes have; one LDS counter per (instance, snapshot).
+// (u8 counters, four per word: a count never exceeds N <= 64, so the add never carries)
 __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
-  const uint32_t old = lds_add(&XW(x.lay.x_done + x.seg * x.lay.s_cap + sid), 1u);
-  if (old + 1 == (uint32_t)x.p.n_nodes) {
+  const uint32_t sh = ((uint32_t)sid & 3u) * 8u;
+  const uint32_t old = lds_add(&XW(x.lay.x_done + x.seg * x.lay.sp + (sid >> 2)), 1u << sh);
+  if (((old >> sh) & 0xffu) + 1 == (uint32_t)x.p.n_nodes) {
     st_snap(x.p.snap_tick, 4u * (x.inst * (uint32_t)x.lay.s_cap + (uint32_t)sid), ln.time);
     lds_add(&XW(x.lay.x_ndone + x.seg), 1u);
   }
@@ -302,14 +311,14 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
                      ln.tokens);
     if (x.outdeg) {
       XW(lay.x_tslot + x.seg_base + src) = (uint32_t)x.outdeg;
-      PW(lay.w_trig + ntrig) = src | ((uint32_t)sid << 8);
+      TRIG(ntrig) = (uint16_t)(src | ((uint32_t)sid << 8));
       ntrig++;
     }
   } else {  // later marker: stop recording this channel
     // hi16 of the cursor word: the channel's end
     st_snap(reinterpret_cast<uint16_t*>(x.p.snap_nod),
           plane_off(x, (uint32_t)sid, x.nod_plane) + nod_lane(x) + 4u * (1 + (uint32_t)ki) + 2u,
-          (uint16_t)PW(lay.w_cur + ki));
+          (uint16_t)CUR(ki));
     pend = ((pw >> sh) & 0xffu) - 1;
   }
   PW(pi) = (pw & ~(0xffu << sh)) | (pend << sh);
@@ -348,8 +357,8 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
     for (int32_t ko = 0; ko < D; ++ko) {
       if (ko >= lay.od) break;  // uniform: the layout holds od out-links per lane
       const bool look = scanning && ko < x.outdeg;
-      const uint32_t chw = PW(lay.w_chw + ko);
-      const uint32_t cnt = (chw >> 8) & 0xffu;
+      const uint32_t chw = CHW(ko);
+      const uint32_t cnt = chw >> 8;
       const uint32_t head = chw & (cap - 1);
       const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
       const uint32_t e = PW(slot);
@@ -358,8 +367,8 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       ln.peek += nonempty ? 1u : 0u;
       const bool due = nonempty && (int32_t)((e >> 16) & 0x7fffu) <= ln.time;
       if (__builtin_expect(due && cnt > cap, 0)) refill(x, ko, slot);
-      const uint32_t popped = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
-      PW(lay.w_chw + ko) = due ? popped : chw;
+      const uint32_t popped = ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
+      CHW(ko) = (uint16_t)(due ? popped : chw);
       pick = due ? ((e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16)) : pick;
       scanning = scanning && !due;
     }
@@ -369,8 +378,8 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
     for (int32_t ko = 0; ko < (unrolled(D) ? D : x.outdeg); ++ko) {
       if (ko >= x.outdeg) break;
       if (done) continue;
-      const uint32_t chw = PW(lay.w_chw + ko);
-      const uint32_t cnt = (chw >> 8) & 0xffu;
+      const uint32_t chw = CHW(ko);
+      const uint32_t cnt = chw >> 8;
       if (!cnt) {
         empty_scanned |= 1u << ko;
         continue;
@@ -381,7 +390,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       const uint32_t e = PW(slot);
       if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) continue;
       if (__builtin_expect(cnt > cap, 0)) refill(x, ko, slot);
-      PW(lay.w_chw + ko) = (chw & 0xffff0000u) + ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
+      CHW(ko) = (uint16_t)(((cnt - 1) << 8) + ((head + 1) & (cap - 1)));
       pick = (e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16);
       done = true;
     }
@@ -407,8 +416,8 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
         if (m) temit<TRACE>(x, mk ? TK_RECV_MARKER : TK_RECV_TOKEN, src, ln.time, src << 8, (int32_t)pay, ln.tokens);
       // HandleToken: tokens += data; the channel's recording cursor advances
       ln.tokens += tok ? (int32_t)pay : 0;
-      const uint32_t cur = PW(lay.w_cur + ki);
-      PW(lay.w_cur + ki) = cur + (tok ? 1u : 0u);
+      const uint32_t cur = CUR(ki);
+      CUR(ki) = (uint16_t)(cur + (tok ? 1u : 0u));
       if (mk) handle_marker<D, TRACE>(x, ln, it, ki, w, src, (int32_t)pay, ntrig);
     }
   } else if (act) {
@@ -424,7 +433,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
                    ln.tokens);
       if (!(pk & kMarkerBit)) {  // HandleToken: tokens += data; the recording cursor advances
         ln.tokens += (int32_t)pay;
-        PW(lay.w_cur + ki) += 1u;
+        CUR(ki) = (uint16_t)(CUR(ki) + 1u);
         continue;
       }
       handle_marker<D, TRACE>(x, ln, it, ki, w, src, (int32_t)pay, ntrig);
@@ -442,7 +451,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
     const uint32_t base = x.seg_base > 0 ? XW(lay.x_off + x.seg_base - 1) : 0u;
     const uint32_t total = XW(lay.x_off + x.seg_base + x.p.n_nodes - 1) - base;
     for (int32_t kk = 0; kk < ntrig; ++kk) {
-      const uint32_t tv = PW(lay.w_trig + kk);
+      const uint32_t tv = TRIG(kk);
       const uint32_t src = tv & 0xffu;
       const uint32_t sid = tv >> 8;
       // exclusive prefix of the triggering sender within the instance
@@ -522,7 +531,7 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
     if (ln.tokens < on || oj < 0 || (int64_t)ln.draw + pos >= x.p.draws) {
       bad = true;
     } else {  // the checks push() makes
-      const uint32_t cnt = (PW(lay.w_chw + oj) >> 8) & 0xffu, cap = 1u << lay.cap_log2;
+      const uint32_t cnt = (uint32_t)CHW(oj) >> 8, cap = 1u << lay.cap_log2;
       bad = cnt >= (uint32_t)kMaxQueued || (cnt >= cap && (lay.ocap_log2 < 0 || cnt - cap >= (1u << lay.ocap_log2)));
     }
   }
@@ -551,54 +560,38 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
 #define CLSNAP_W2 0
 #endif
 #ifndef CLSNAP_W4
-#define CLSNAP_W4 5  // D = 4 (8nodes-concurrent, BASELINE config 3): 5 waves/SIMD, DESIGN.md §9
+#define CLSNAP_W4 5  // D = 3, 4 with HBM spill rings: 5 waves/SIMD, DESIGN.md §9
 #endif
-constexpr int waves_for(int D) {
-  return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1)
-         : (D == 3 || D == 4) ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : 1;
+#ifndef CLSNAP_FIXUP
+#define CLSNAP_FIXUP 1  // A/B knob: 0 runs fresh full runs with spill rings on the spill-capable kernel
+#endif
+#ifndef CLSNAP_W4NS
+#define CLSNAP_W4NS 6  // D = 3, 4 spill-free (the main pass of BASELINE config 3): 6 waves/SIMD
+#endif
+// The spill fix-up runs few waves, each latency-bound through a whole instance: it takes
+// registers over occupancy (2 waves per SIMD: no scratch spills in the tick loop).
+constexpr int waves_for(int D, bool spill, bool fixup) {
+  return fixup ? 2
+         : D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1)
+         : (D == 3 || D == 4) ? (spill ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : CLSNAP_W4NS) : 1;
 }
 
-// CAP > 0: the layout's private column is ColumnC<D, CAP> (compile-time offsets: register
-// pressure of the D = 3 kernel 95 VGPRs + 58 SGPR spills -> ~80 VGPRs, no spills); SPILL false
-// compiles out the HBM spill rings (a layout without them).  CAP = 0 reads every offset from
-// the runtime layout (any D, any ring size).
-template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_kernel(ExecParams p, const uint32_t* __restrict__ topo,
-                                                                         const Op* __restrict__ ops,
-                                                                         const uint8_t* __restrict__ sched) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  Layout lay_ = p.lay;
-  if constexpr (CAP > 0) {
-    using Col = ColumnC<D, CAP>;
-    lay_.cap_log2 = CAP;
-    lay_.od = lay_.id = D;
-    lay_.w_fifo = Col::w_fifo;
-    lay_.w_chw = Col::w_chw;
-    lay_.w_cur = Col::w_cur;
-    lay_.w_int = Col::w_int;
-    lay_.w_trig = Col::w_trig;
-    lay_.w_pend = Col::w_pend;
-    if constexpr (!SPILL) lay_.ocap_log2 = -1;
-    lay_.x_pick = 0;
-    lay_.x_tslot = kWave;
-    lay_.x_off = 2 * kWave;
-    lay_.x_done = 3 * kWave;
-  }
-  const Layout& lay = lay_;
+// The whole event program for the instances of one wave (slots wave * ipw .. + ipw - 1 of
+// the launch; n_slots slots in all).  Every lane of the wave must call it.
+template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED, bool FIXUP>
+__device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay, uint32_t wave, uint32_t n_slots,
+                                          const int32_t* imap, lds_u32* X, const uint32_t* __restrict__ topo,
+                                          const Op* __restrict__ ops, const uint8_t* __restrict__ sched) {
   const int32_t N = p.n_nodes;
   const int32_t lane = threadIdx.x & (kWave - 1);
-  const int32_t wib = threadIdx.x / kWave;
-  const uint32_t wave = blockIdx.x * (uint32_t)p.lay.wpb + wib;
-  lds_u32* X = (lds_u32*)(lds + (size_t)wib * lay.wave_words);
   const int32_t seg = lane / N;
   const int32_t v = lane - seg * N;
-  // slot = position in the launch; inst = the instance it runs (p.inst_map: replays grouped
-  // by length so a wave's segments finish together, cl_host.cpp)
+  // slot = position in the launch; inst = the instance it runs (imap: replays grouped by
+  // length so a wave's segments finish together, or the spill fix-up's worklist, cl_host.cpp)
   // (MAPPED: specialized kernels launch with a map, the others without; the generic CAP = 0
   // kernel checks at run time)
-  const int32_t* imap = MAPPED ? p.inst_map : nullptr;
   const uint32_t slot = wave * (uint32_t)lay.ipw + seg;
-  const bool valid = seg < lay.ipw && slot < p.n_inst;
+  const bool valid = seg < lay.ipw && slot < n_slots;
   const uint32_t inst = ((CAP > 0 || imap) && MAPPED && valid) ? (uint32_t)imap[slot] : slot;
   const uint32_t ii = valid ? inst : 0u;  // safe index for lanes without an instance
   const uint32_t* nb = topo + (size_t)(valid ? v : 0) * p.topo_w;
@@ -609,7 +602,7 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   const lds_u8* lrow = STAGED ? (const lds_u8*)(X + lay.x_delay) + (size_t)seg * p.sched_row : nullptr;
   if constexpr (STAGED) {
     const uint32_t first = wave * (uint32_t)lay.ipw;
-    const uint32_t nrow = min((uint32_t)lay.ipw, (uint32_t)p.n_inst - min(first, (uint32_t)p.n_inst));
+    const uint32_t nrow = min((uint32_t)lay.ipw, n_slots - min(first, n_slots));
     const uint32_t rw4 = (uint32_t)(p.sched_row / 4);
     if (!MAPPED || (CAP == 0 && !imap)) {  // consecutive instances: one contiguous copy
       const uint32_t words = nrow * rw4;
@@ -669,7 +662,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     wave_sync();
     if (valid && v == 0) {
       const uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
-      for (int32_t s = 0; s < lay.s_cap; ++s) XW(lay.x_done + seg * lay.s_cap + s) = Dn[s * st];
+      for (int32_t q = 0; q < lay.sp; ++q) {
+        uint32_t w = 0;
+        for (int32_t b = 0; b < 4; ++b) w |= (Dn[(4 * q + b) * st] & 0xffu) << (8 * b);
+        XW(lay.x_done + seg * lay.sp + q) = w;
+      }
       XW(lay.x_ndone + seg) = Dn[lay.s_cap * st];
     }
   }
@@ -745,8 +742,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   {
     const uint32_t cap = 1u << lay.cap_log2;
     for (int32_t ko = 0; ko < outdeg; ++ko) {
-      const uint32_t chw = PW(lay.w_chw + ko);
-      const uint32_t cnt = (chw >> 8) & 0xffu, head = chw & 0xffu;
+      const uint32_t chw = CHW(ko);
+      const uint32_t cnt = chw >> 8, head = chw & 0xffu;
       for (uint32_t k = 0; k < cnt && k < cap; ++k) {
         const uint32_t e = PW(lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + ((head + k) & (cap - 1)));
         if (!(e & kMarkerBit)) inflight += (int32_t)(e & 0xffffu);
@@ -792,6 +789,11 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
     r[R_POP_MK] = (int32_t)acc[2];
     r[R_PUSH] = (int32_t)acc[3];
     r[R_INFLIGHT_TOK] = (int32_t)acc[4];
+    // spill-free main pass: an instance frozen by a full LDS ring (or a queue past 255) is
+    // re-run from the initial state by the spill fix-up launch, which either spills it to
+    // HBM or freezes it with the same status at the same push
+    if constexpr (!SPILL && !FIXUP)
+      if (p.fix_list && ln.status == ST_FIFO_OVERFLOW) p.fix_list[atomicAdd(p.fix_count, 1u)] = ii;
   }
   if (!p.save_state) return;
   uint32_t* S = p.state + ii;
@@ -809,8 +811,55 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D)) void cl_exec_
   R[G_PUSH * st] = ln.push;
   if (v == 0) {
     uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
-    for (int32_t s = 0; s < lay.s_cap; ++s) Dn[s * st] = XW(lay.x_done + seg * lay.s_cap + s);
+    for (int32_t s = 0; s < lay.s_cap; ++s) Dn[s * st] = (XW(lay.x_done + seg * lay.sp + (s >> 2)) >> ((s & 3) * 8)) & 0xffu;
     Dn[lay.s_cap * st] = XW(lay.x_ndone + seg);
+  }
+}
+
+// CAP > 0: the layout's private column is ColumnC<D, CAP> (compile-time offsets: register
+// pressure of the D = 3 kernel 95 VGPRs + 58 SGPR spills -> ~80 VGPRs, no spills); SPILL false
+// compiles out the HBM spill rings.  CAP = 0 reads every offset from the runtime layout (any
+// D, any ring size).  FIXUP: the spill fix-up -- persistent waves over the worklist the
+// spill-free main pass filled (p.fix_list, *p.fix_count entries); it also zeroes the other
+// counter of the pair (p.fix_clear) for the next main pass.  Every wave exits once the list
+// is exhausted.
+template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED, bool FIXUP = false>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D, SPILL, FIXUP)) void cl_exec_kernel(
+    ExecParams p, const uint32_t* __restrict__ topo, const Op* __restrict__ ops, const uint8_t* __restrict__ sched) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  Layout lay_ = p.lay;
+  if constexpr (CAP > 0) {
+    using Col = ColumnC<D, CAP>;
+    lay_.cap_log2 = CAP;
+    lay_.od = lay_.id = D;
+    lay_.w_fifo = Col::w_fifo;
+    lay_.w_lnk = Col::w_lnk;
+    lay_.w_int = Col::w_int;
+    lay_.w_trig = Col::w_trig;
+    lay_.w_pend = Col::w_pend;
+    if constexpr (!SPILL) lay_.ocap_log2 = -1;
+    lay_.x_pick = 0;
+    lay_.x_tslot = kWave;
+    lay_.x_off = 2 * kWave;
+    lay_.x_done = 3 * kWave;
+  }
+  const Layout& lay = lay_;
+  const int32_t wib = threadIdx.x / kWave;
+  lds_u32* X = (lds_u32*)(lds + (size_t)wib * lay.wave_words);
+  if constexpr (FIXUP) {
+    static_assert(MAPPED && SPILL, "the fix-up re-runs listed instances with spill rings");
+    const uint32_t n = *p.fix_count;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *p.fix_clear = 0u;
+    const uint32_t nw = (n + (uint32_t)lay.ipw - 1) / (uint32_t)lay.ipw;
+    for (uint32_t w = blockIdx.x * (uint32_t)p.lay.wpb + wib; w < nw; w += gridDim.x * (uint32_t)p.lay.wpb) {
+      wave_sync();
+      exec_wave<D, STAGED, TRACE, CAP, SPILL, MAPPED, FIXUP>(p, lay, w, n, reinterpret_cast<const int32_t*>(p.fix_list),
+                                                             X, topo, ops, sched);
+    }
+  } else {
+    exec_wave<D, STAGED, TRACE, CAP, SPILL, MAPPED, FIXUP>(p, lay, blockIdx.x * (uint32_t)p.lay.wpb + wib,
+                                                           (uint32_t)p.n_inst, MAPPED ? p.inst_map : nullptr, X, topo,
+                                                           ops, sched);
   }
 }
 
@@ -871,28 +920,172 @@ __global__ __launch_bounds__(256) void cl_checksum_kernel(SumParams p) {
     if (v[k]) atomicAdd(&p.out[k], v[k]);
 }
 
+// Recorded copies over completed snapshots, all instances / OK instances (cl_get_counters).
+__global__ __launch_bounds__(256) void cl_recorded_kernel(SumParams p) {
+  const int64_t inst = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long rec = 0;
+  bool ok = false;
+  if (inst < p.n_inst) {
+    ok = p.regs[inst * R_NUM + R_STATUS] == ST_OK;
+    for (int32_t sid = 0; sid < p.n_sids; ++sid) {
+      if (p.snap_tick[inst * p.s_cap + sid] < 0) continue;
+      const uint32_t* rb = p.snap_nod + ((int64_t)sid * p.stride + inst) * p.n_nodes * p.rw;
+      for (int32_t c = 0; c < p.n_ch; ++c) {
+        const uint32_t r = rb[p.ch_slot[c]];
+        rec += (r >> 16) - (r & 0xffffu);
+      }
+    }
+  }
+  unsigned long long a = rec, b = ok ? rec : 0;
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b += __shfl_xor(b, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (a) atomicAdd(&p.out[0], a);
+    if (b) atomicAdd(&p.out[1], b);
+  }
+}
+
+// ---- CollectSnapshot packed on the device (PackParams) ------------------------------
+// count: one thread per instance -- tokenMap entries, completion flag, and the number of
+// recorded messages over the channels (the cursor intervals' lengths).
+__global__ __launch_bounds__(256) void cl_pack_count(PackParams p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const int64_t inst = p.lo + i;
+  const bool done = p.snap_tick[inst * p.s_cap + p.sid] >= 0;
+  const uint32_t* rb = p.snap_nod + ((int64_t)p.sid * p.stride + inst) * p.n_nodes * p.rw;
+  long long cnt = 0;
+  for (int32_t v = 0; v < p.n_nodes; ++v) p.tokens[i * p.n_nodes + v] = done ? (int32_t)rb[(int64_t)v * p.rw] : -1;
+  if (done)
+    for (int32_t c = 0; c < p.n_ch; ++c) {
+      const uint32_t r = rb[p.ch_slot[c]];
+      cnt += (long long)((r >> 16) - (r & 0xffffu));
+    }
+  p.complete[i] = done ? 1 : 0;
+  p.count[i] = cnt;
+}
+
+// Exclusive scan of count[0, n) in place (count[n] = total): block-local scans of kScanItems
+// entries (256 threads x 8, wave shuffles), a one-workgroup scan of the block sums, an add.
+__device__ __forceinline__ long long block_scan_excl(long long x, long long* sh, long long* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  long long inc = x;
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  long long pre = 0, tot = 0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+    if (k < w) pre += sh[k];
+    tot += sh[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc - x;
+}
+
+__global__ __launch_bounds__(256) void cl_scan_blocks(long long* a, int64_t n, long long* bsum) {
+  __shared__ long long sh[4];
+  const int64_t base = (int64_t)blockIdx.x * kScanItems + threadIdx.x * 8;
+  long long v[8], s = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    v[q] = base + q < n ? a[base + q] : 0;
+    s += v[q];
+  }
+  long long tot;
+  long long pre = block_scan_excl(s, sh, &tot);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if (base + q < n) a[base + q] = pre;
+    pre += v[q];
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void cl_scan_top(long long* bsum, int64_t nb, long long* total) {
+  __shared__ long long sh[4];
+  long long carry = 0;
+  for (int64_t c0 = 0; c0 < nb; c0 += 256) {
+    const int64_t k = c0 + threadIdx.x;
+    const long long x = k < nb ? bsum[k] : 0;
+    long long tot;
+    const long long pre = block_scan_excl(x, sh, &tot);
+    if (k < nb) bsum[k] = carry + pre;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void cl_scan_add(long long* a, int64_t n, const long long* bsum) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] += bsum[i / kScanItems];
+}
+
+// fill: one thread per instance -- its channel offsets and its messages, channel by channel
+// in delivery order (the token history interval [begin, end) of each recording cursor).
+__global__ __launch_bounds__(256) void cl_pack_fill(PackParams p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) p.offsets[p.n * p.n_ch] = p.count[p.n];
+  if (i >= p.n) return;
+  const int64_t inst = p.lo + i;
+  const bool done = p.complete[i] != 0;
+  const uint32_t* rb = p.snap_nod + ((int64_t)p.sid * p.stride + inst) * p.n_nodes * p.rw;
+  long long m = p.count[i];
+  long long* off = p.offsets + i * p.n_ch;
+  for (int32_t c = 0; c < p.n_ch; ++c) {
+    off[c] = m;
+    if (!done) continue;
+    const uint32_t r = rb[p.ch_slot[c]];
+    const int32_t* hv = p.hist_val + p.hist_off[c];
+    for (uint32_t k = r & 0xffffu; k < (r >> 16); ++k) p.msgs[m++] = hv[k];
+  }
+}
+
 #endif
 
 }  // namespace
 
-template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true>
+template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true, bool FIXUP = false>
 int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
   const int32_t wpb = p.lay.wpb;
   const size_t lds = (size_t)p.lay.wave_words * wpb * sizeof(uint32_t);
+  auto* k = cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED, FIXUP>;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       kMaxLdsBytes);
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
   const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
-  const unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
-  hipExtLaunchKernelGGL((cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>), dim3(blocks), dim3(kWave * wpb), lds,
-                        (hipStream_t)L.stream, (hipEvent_t)L.ev_start, (hipEvent_t)L.ev_stop, 0u, p, topo, ops, sched);
+  const unsigned blocks = FIXUP ? (unsigned)p.fix_blocks : (unsigned)((waves + wpb - 1) / wpb);
+  hipExtLaunchKernelGGL(k, dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)L.stream, (hipEvent_t)L.ev_start,
+                        (hipEvent_t)L.ev_stop, 0u, p, topo, ops, sched);
   return (int)hipGetLastError();
 }
 
+// A fresh full run with the spill fix-up: the spill-free main pass (6 waves per SIMD for D =
+// 3, 4: smaller register and LDS footprint), then the spill-capable kernel over the instances
+// it froze.  The dispatches record the start (main) and stop (fix-up) events.
+template <int D, int CAP, bool MAPPED>
+int launch_exec_fixup(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched,
+                      const ExecLaunch& L) {
+  ExecLaunch a = L, b = L;
+  a.ev_stop = nullptr;
+  b.ev_start = nullptr;
+  int e = launch_exec_ds<D, true, false, CAP, false, MAPPED>(p, topo, ops, sched, a);
+  if (e) return e;
+  if (L.fixup_launched) *L.fixup_launched = 1;
+  return launch_exec_ds<D, true, false, CAP, true, true, true>(p, topo, ops, sched, b);
+}
+
 template <int D>
-int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
+int launch_exec_d(const ExecParams& pf, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
+  // (only the specialized spill-free main pass appends to the fix-up worklist)
+  ExecParams p = pf;
+  p.fix_list = nullptr;
   // The trace build reads delays from HBM (one instantiation per D, debug runs only).
   if (p.trace_n > 0) return launch_exec_ds<D, false, true>(p, topo, ops, sched, L);
   if constexpr (unrolled(D)) {
@@ -900,12 +1093,18 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
     // specialized on the column layout, with or without HBM spill rings
     const bool ok = p.lay.od == D && p.lay.id == D;
     if (p.lay.x_delay > 0 && ok) {
-      const bool sp = p.lay.ocap_log2 >= 0 && !p.nospill;
+      // spill rings in the layout: a fresh full run takes the spill-free main pass and the
+      // fix-up; a resumed launch (state may hold spilled queues) the spill-capable kernel
+      const bool rings = p.lay.ocap_log2 >= 0;
+      const bool fix = CLSNAP_FIXUP && rings && pf.fix_list != nullptr;
+      if (fix) p.fix_list = pf.fix_list;
       const bool mp = p.inst_map != nullptr;
 #define CLSNAP_SPEC(C)                                                                              \
   case C:                                                                                           \
-    if (sp) return mp ? launch_exec_ds<D, true, false, C, true, true>(p, topo, ops, sched, L)   \
-                      : launch_exec_ds<D, true, false, C, true, false>(p, topo, ops, sched, L); \
+    if (fix) return mp ? launch_exec_fixup<D, C, true>(p, topo, ops, sched, L)                  \
+                       : launch_exec_fixup<D, C, false>(p, topo, ops, sched, L);                \
+    if (rings) return mp ? launch_exec_ds<D, true, false, C, true, true>(p, topo, ops, sched, L)   \
+                         : launch_exec_ds<D, true, false, C, true, false>(p, topo, ops, sched, L); \
     return mp ? launch_exec_ds<D, true, false, C, false, true>(p, topo, ops, sched, L)          \
               : launch_exec_ds<D, true, false, C, false, false>(p, topo, ops, sched, L);
       switch (p.lay.cap_log2) {
@@ -971,6 +1170,34 @@ extern "C" int cl_prof_read(unsigned long long* out, int reset) {
 int launch_checksums(const SumParams& p, void* stream) {
   const unsigned blocks = (unsigned)((p.n_inst + 255) / 256);
   hipLaunchKernelGGL(cl_checksum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p);
+  return (int)hipGetLastError();
+}
+
+int launch_recorded(const SumParams& p, void* stream) {
+  const unsigned blocks = (unsigned)((p.n_inst + 255) / 256);
+  hipLaunchKernelGGL(cl_recorded_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p);
+  return (int)hipGetLastError();
+}
+
+int launch_pack_count(const PackParams& p, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (p.n > 0) {
+    hipLaunchKernelGGL(cl_pack_count, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, p);
+    const int64_t nb = (p.n + kScanItems - 1) / kScanItems;
+    hipLaunchKernelGGL(cl_scan_blocks, dim3((unsigned)nb), dim3(256), 0, s, p.count, p.n, p.bsum);
+    hipLaunchKernelGGL(cl_scan_top, dim3(1), dim3(256), 0, s, p.bsum, nb, p.count + p.n);
+    hipLaunchKernelGGL(cl_scan_add, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, p.count, p.n,
+                       (const long long*)p.bsum);
+  } else {
+    hipError_t e = hipMemsetAsync(p.count, 0, sizeof(long long), s);
+    if (e != hipSuccess) return (int)e;
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_pack_fill(const PackParams& p, void* stream) {
+  const unsigned blocks = (unsigned)((p.n + 255) / 256);
+  hipLaunchKernelGGL(cl_pack_fill, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, (hipStream_t)stream, p);
   return (int)hipGetLastError();
 }
 

@@ -143,11 +143,14 @@ int cl_last_kernel_ms(cl_sim* sim, double* ms);
 /* Sum of exec-kernel device times (HIP events around every launch) since the previous
  * call, and the number of launches; resets the accumulator. */
 int cl_kernel_time(cl_sim* sim, double* total_ms, int64_t* launches);
-/* 1 in *on when the next cl_rerun runs the spill-free kernel: a fresh run of the same program
- * with the same delays and layout already completed without pushing onto an HBM spill ring,
- * so its replays fill the same LDS queues (engine-internal specialization; results are the
- * same either way). */
+/* 1 in *on when the next cl_rerun's main pass runs the spill-free kernel: the layout has no
+ * HBM spill rings, or the engine's specialized kernels serve it -- a fresh full run then
+ * runs every instance spill-free and re-runs only those whose LDS rings overflowed with the
+ * spill rings (the spill fix-up; engine-internal, results are the same either way). */
 int cl_replay_spill_free(cl_sim* sim, int32_t* on);
+/* Instances the spill fix-up of the latest launch re-ran with HBM spill rings (0 when that
+ * launch had no fix-up). */
+int cl_fixup_instances(cl_sim* sim, int64_t* n);
 /* 1 in *on when the next cl_rerun launches through the length-ordered slot map (instances
  * grouped by the final tick of an earlier full run of the same program and delays, so the
  * instances sharing a wave finish together; engine-internal, results unchanged). */
@@ -211,6 +214,21 @@ int cl_wait_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi,
  * written) if msg_cap is too small. */
 int cl_collect_snapshot_range(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int64_t* tokens,
                               int32_t* complete, int64_t* msg_offsets, int64_t* msg_tokens, int64_t msg_cap);
+/* CollectSnapshot (sim.go:134-173; finalizeSnapshot node.go:188-195) of instances
+ * [inst_lo, inst_hi), packed on the GPU: only the packed arrays cross PCIe.
+ *   tokens[(i - inst_lo) * N + rank]    tokenMap (int32), -1 where not complete
+ *   complete[i - inst_lo]                1 when the snapshot completed in instance i
+ *   msg_offsets[r * C + c]               start of instance r's channel c (int64, (hi-lo)*C+1
+ *                                        entries; channels in (src rank, dest rank) order)
+ *   msg_tokens[...]                      recorded token counts (int32), delivery order
+ * Any output pointer may be NULL; *n_msgs (may be NULL) = messages; CL_E_LIMIT (everything
+ * else still written) when msg_cap is too small.  cl_collect_snapshot_range is the same
+ * collect with int64 tokens and messages (widened on the host). */
+int cl_collect_snapshot_packed(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi, int32_t* tokens,
+                               int32_t* complete, int64_t* msg_offsets, int32_t* msg_tokens, int64_t msg_cap,
+                               int64_t* n_msgs);
+/* Device time of the latest packed collect's kernels (HIP events). */
+int cl_collect_time(cl_sim* sim, double* device_ms);
 /* Counters over instances (only_ok: restrict to CL_INST_OK instances). */
 int cl_get_counters(cl_sim* sim, int32_t only_ok, int64_t* out /* [CL_NUM_COUNTERS] */);
 /* Batch checksums computed on the GPU (see CL_SUM_*); all-reduce them across ranks. */

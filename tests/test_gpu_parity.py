@@ -251,8 +251,12 @@ def test_rerun_equals_flush_and_oracle(cfg):
     top, events, n, slots = cfg
     sim = engine_run(top, events, n, fifo_lds_slots=slots)
     first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
-    if slots == 2:  # two LDS slots: deep channels must have used the HBM spill rings
-        assert not sim.spill_free_replays()
+    # the main pass runs spill-free; instances whose LDS rings overflow are re-run with the
+    # HBM spill rings by the fix-up -- with two LDS slots, deep channels must need them
+    assert sim.spill_free_replays()
+    fixed = sim.fixup_instances()
+    if slots == 2:
+        assert fixed > 0
     if n == 131072 and slots is None:  # C3: instance lengths spread (13..50 ticks): mapped replays
         assert sim.mapped_replays()
     if n == 65536:  # C2: too little spread to pay for the map
@@ -268,6 +272,7 @@ def test_rerun_equals_flush_and_oracle(cfg):
         sim.poison_outputs()      # results below can only come from this rerun
         sim.rerun()
         sim.synchronize()
+        assert sim.fixup_instances() == fixed, f"rerun {r}: fix-up worklist"
         status, times, sums = sim.status(), sim.time(), sim.checksums()
         assert np.array_equal(status, first[0]) and np.array_equal(status, st), f"rerun {r}: status"
         assert np.array_equal(times, first[1]), f"rerun {r}: times"
@@ -283,12 +288,15 @@ def test_rerun_equals_flush_and_oracle(cfg):
                          status=status, times=times)
 
 
-def test_spill_free_replay_after_probe():
-    """A flush that never needs an HBM spill ring lets reruns take the spill-free kernel
-    (cl_replay_spill_free); appending events invalidates that until the next full run, and
-    every rerun equals the flush and the oracle."""
-    # A->B carries a send and two markers (depth bound 3 > 2 LDS slots: spill rings are
-    # provisioned), but the ticks between them keep at most one packet queued
+def test_spill_fixup_reruns_exactly_the_overflowing_instances():
+    """A fresh full run runs every instance spill-free; an instance whose push finds its
+    LDS ring full freezes with FIFO_OVERFLOW and is listed, and the fix-up launch re-runs
+    exactly the listed instances from the initial state with the HBM spill rings.  Two LDS
+    slots: A->B carries a send and two markers; with ticks between them the queue never
+    holds more than two packets, so nothing needs the fix-up -- until appended events queue
+    five tokens at once on A->B.  Every launch equals the oracle, incremental flushes
+    (spill-capable resumed launches) included, and the worklist counters alternate cleanly
+    across launches."""
     top = "3\nA 10\nB 10\nC 10\nA B\nB C\nC A\nB A\n"
     ev = "send A B 2\ntick 6\nsnapshot A\ntick 6\nsnapshot B\n"
     n = 512
@@ -296,28 +304,41 @@ def test_spill_free_replay_after_probe():
     sim.read_topology_text(top)
     sim.read_events_text(ev)
     sim.flush()
+    assert sim.spill_free_replays() and sim.fixup_instances() == 0
     first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
-    assert sim.spill_free_replays()
     for i in range(0, n, 37):
         compare_instance(sim, i, oracle_run(top, ev, seed=O.REFERENCE_SEED + i), status=first[0], times=first[1])
     for _ in range(2):
         sim.poison_outputs()
         sim.rerun()
         sim.synchronize()
+        assert sim.fixup_instances() == 0
         assert np.array_equal(sim.status(), first[0]) and np.array_equal(sim.time(), first[1])
         assert np.array_equal(sim.checksums(), first[2])
     ev2 = "send A B 1\nsend A B 1\nsend A B 1\nsend A B 1\nsend A B 1\ntick 1\n"
     sim.read_events_text(ev2)
-    assert not sim.spill_free_replays()  # (the longer program has not run in full yet)
-    sim.rerun()
-    sim.synchronize()
-    ref = cl.ChandyLamportSim(n, fifo_lds_slots=2)  # the same two readEventsFile calls, one flush
-    ref.read_topology_text(top)
-    ref.read_events_text(ev)
-    ref.read_events_text(ev2)
-    ref.flush()
-    assert np.array_equal(sim.status(), ref.status()) and np.array_equal(sim.time(), ref.time())
-    assert np.array_equal(sim.checksums(), ref.checksums())
+    sim.flush()                   # (after reruns: a fresh full run) every instance overflows
+    assert sim.fixup_instances() == n
+    ev3 = "send B A 1\nsend A B 1\ntick 2\n"
+    sim.read_events_text(ev3)
+    sim.flush()                   # resumed launch: the spill-capable kernel, no fix-up
+    assert sim.fixup_instances() == 0
+    inc = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
+    for r in range(3):
+        sim.poison_outputs()
+        sim.rerun()               # fresh full run: every instance overflows two LDS slots
+        sim.synchronize()
+        assert sim.fixup_instances() == n, f"rerun {r}"
+        assert np.array_equal(sim.status(), inc[0]) and np.array_equal(sim.time(), inc[1])
+        assert np.array_equal(sim.checksums(), inc[2])
+    for i in range(0, n, 37):
+        o = O.OracleSim()
+        o.seed_go(O.REFERENCE_SEED + i)
+        assert o.read_topology_text(top) == 0
+        o.read_events_text(ev)
+        o.read_events_text(ev2)
+        o.read_events_text(ev3)
+        compare_instance(sim, i, o, status=inc[0], times=inc[1])
 
 
 def test_headline_batch_2p20_matches_fixture():
@@ -374,3 +395,53 @@ def test_two_event_texts_and_snapshot_after_drain():
     sim.synchronize()
     assert np.array_equal(sim.status(), first[0]) and np.array_equal(sim.time(), first[1])
     assert np.array_equal(sim.checksums(), first[2])
+
+
+def test_packed_collect_equals_host_expansion_and_oracle():
+    """CollectSnapshot packed on the GPU (cl_collect_snapshot_packed: node records expanded
+    over the channels' token histories into one CSR over (instance, channel), finalizeSnapshot
+    node.go:188-195 / CollectSnapshot sim.go:134-173) equals the host expansion of each
+    instance's records (cl_collect_snapshot) and the oracle, on the C3 batch: every snapshot,
+    a sub-range that starts mid-batch, and totals that match the recorded-copy counter."""
+    top, events, n = "8nodes.top", "8nodes-concurrent-snapshots.events", 65536
+    sim = engine_run(top, events, n)
+    status = sim.status()
+    ids, chans = sim.node_ids(), sim.channels()
+    C = len(chans)
+    total = 0
+    rng = np.random.default_rng(5)
+    sample = np.concatenate([[0, 1, n - 1], rng.choice(n, 40, replace=False), np.nonzero(status != 0)[0][:8]])
+    refs = {int(i): oracle_run(top, events, seed=O.REFERENCE_SEED + int(i)) for i in sample}
+    for sid in range(sim.num_snapshots):
+        tok, done, off, msg = sim.collect_snapshot_packed(sid)
+        assert off[0] == 0 and np.all(np.diff(off) >= 0) and off[-1] == msg.size
+        total += msg.size
+        ticks = np.array([sim.snapshot_tick(sid, int(i)) for i in sample])
+        assert np.array_equal(done[sample], ticks >= 0)
+        for i, t in zip(sample, ticks):
+            i = int(i)
+            if t < 0:
+                assert (tok[i] == -1).all() and off[i * C] == off[(i + 1) * C]
+                continue
+            g = sim.CollectSnapshot(sid, i)                    # host expansion of the records
+            assert dict(zip(ids, tok[i].tolist())) == g.tokenMap
+            got = {}
+            for c in range(C):
+                for k in range(off[i * C + c], off[i * C + c + 1]):
+                    got.setdefault((ids[chans[c][0]], ids[chans[c][1]]), []).append(int(msg[k]))
+            assert got == canonical(g.messages)
+            ref = refs[i]
+            if ref.status == 0 or ref.complete(sid):
+                w = ref.collect(sid)
+                assert g.tokenMap == w.tokens and canonical(g.messages) == canonical(w.messages)
+        # a sub-range equals the same slice of the whole-batch CSR
+        lo, hi = 12345, 40000
+        t2, d2, o2, m2 = sim.collect_snapshot_packed(sid, lo, hi)
+        assert np.array_equal(t2, tok[lo:hi]) and np.array_equal(d2, done[lo:hi])
+        assert np.array_equal(o2, off[lo * C:hi * C + 1] - off[lo * C])
+        assert np.array_equal(m2, msg[off[lo * C]:off[hi * C]])
+        rt, rd, ro, rm = sim.collect_snapshot_range(sid, lo, hi)    # the int64 form
+        assert np.array_equal(rt, t2) and np.array_equal(rd, d2) and np.array_equal(ro, o2)
+        assert np.array_equal(rm, m2)
+    assert total == sim.counters(only_ok=False)["recorded"]
+    assert sim.collect_time() > 0
