@@ -194,8 +194,9 @@ def main():
     # checksums of the LAST timed rerun (the timed path itself), all-reduced over ranks
     sums = sim.checksums()
     recorded_ok = sim.counters(only_ok=True)["recorded"]
-    replay = {"slot_map": sim.mapped_replays(), "spill_free_main_pass": sim.spill_free_replays(),
-              "fixup_instances": sim.fixup_instances()}
+    spilled, split = sim.replay_split()
+    replay = {"slot_map": sim.mapped_replays(), "spill_free": sim.spill_free_replays(),
+              "spilled_instances": spilled, "split_slot": split}
     fresh = fresh_run(cl, per_rank, device, seed_base + total, top, events, args) if not args.no_fresh else None
     t_max, red = cldist.reduce_results(elapsed, sums.tolist() + [recorded_ok], coll_dev)
     tot = dict(zip(cl.SUM_NAMES, red[:len(cl.SUM_NAMES)]))
@@ -284,9 +285,10 @@ def main():
             "replay": dict(replay, note="value is the replay rate: the timed steps re-run the same "
                                         "program and delays, launched through the slot map that the "
                                         "first run's final ticks give (DESIGN.md section 6); fresh_run is "
-                                        "the first launch on new seeds, with no map; every launch is the "
-                                        "spill-free main pass plus the spill fix-up of fixup_instances "
-                                        "instances (section 5), both inside kernel_ms"),
+                                        "the first launch on new seeds, with no map; split replays run "
+                                        "slots [0, split_slot) on the spill-free kernel and the instances "
+                                        "that spilled in the first run on the spill-capable one, "
+                                        "concurrently (section 5), both inside kernel_ms"),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": hbm_frac,
                          "traffic": traffic, "kernel": "cl_exec_kernel",

@@ -85,7 +85,7 @@ def lib():
         "cl_replay_spill_free": [vp, vp],
         "cl_replay_mapped": [vp, vp],
         "cl_debug_poison_outputs": [vp],
-        "cl_fixup_instances": [vp, vp],
+        "cl_replay_split": [vp, vp, vp],
         "cl_num_nodes": [vp, vp],
         "cl_node_id": [vp, i32, vp],
         "cl_num_channels": [vp, vp],
@@ -404,15 +404,15 @@ class ChandyLamportSim:
         _check(self._L.cl_last_kernel_ms(self._h, C.byref(ms)))
         return ms.value
 
-    def fixup_instances(self):
-        """Instances the latest launch's spill fix-up re-ran with HBM spill rings."""
-        v = C.c_int64(0)
-        _check(self._L.cl_fixup_instances(self._h, C.byref(v)))
-        return v.value
+    def replay_split(self):
+        """(instances that spilled in the probe run, -1 before it; first slot of the
+        spill-capable part of split replays, 0 = no split) -- cl_replay_split."""
+        a, b = C.c_int64(0), C.c_int64(0)
+        _check(self._L.cl_replay_split(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def spill_free_replays(self):
-        """True when the next rerun()'s main pass runs the spill-free kernel (the rest
-        goes through the spill fix-up; cl_replay_spill_free)."""
+        """True when the next rerun() runs wholly on the spill-free kernel (cl_replay_spill_free)."""
         v = C.c_int32(0)
         _check(self._L.cl_replay_spill_free(self._h, C.byref(v)))
         return bool(v.value)

@@ -233,15 +233,15 @@ struct ExecParams {
   int32_t* snap_tick;  // [stride][S_cap]      completion tick or -1 (one row per instance)
   uint32_t* ovf;       // [C][1 << ocap_log2] spill ring
   uint32_t* ovh;       // [C] spill ring head
-  // Spill fix-up (fresh full runs whose layout has spill rings; cl_kernels.hip launch_exec):
-  // the main pass runs the spill-free kernel and appends every instance it froze with
-  // FIFO_OVERFLOW to fix_list; a second launch re-runs exactly those instances from the
-  // initial state with the spill-capable kernel, and zeroes fix_clear (the counter the next
-  // main pass appends to).  nullptr: no fix-up (resumed launches, trace runs).
-  uint32_t* fix_list;  // [n_inst] instances to re-run
-  uint32_t* fix_count; // entries of fix_list
-  uint32_t* fix_clear; // the other counter of the pair
-  int32_t fix_blocks;  // fix-up grid (persistent waves over the list)
+  // Replay plan (cl_host.cpp build_plan, from the first full run of the same program and
+  // delays): nospill -- no instance ever spilled, every launch may take the spill-free
+  // kernel; split_slot > 0 -- the slot map puts the spilling instances last and slots
+  // [split_slot, n_inst) run on the spill-capable kernel, concurrently.  spill_flag (probe
+  // runs): set to 1 for every instance a push spilled to HBM.
+  int32_t nospill;
+  uint32_t slot_base;  // first slot of this launch's grid
+  int64_t split_slot;
+  uint8_t* spill_flag;  // [n_inst] or nullptr
   // slot -> instance for a replay (nullptr: slot i runs instance i).  cl_host orders a
   // replay's instances by their final tick so the segments of a wave finish together
   const int32_t* inst_map;
@@ -280,7 +280,9 @@ struct ExecLaunch {
   void* stream;
   void* ev_start;
   void* ev_stop;
-  int32_t* fixup_launched;  // out: 1 when a spill fix-up launch followed the main pass
+  void* stream2;  // split replays: the spill-capable part runs here (fork / join events)
+  void* ev_fork;
+  void* ev_join;
 };
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
 int launch_checksums(const SumParams& p, void* stream);

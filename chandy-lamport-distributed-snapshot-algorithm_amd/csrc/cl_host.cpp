@@ -50,8 +50,7 @@ const char* last_error() { return g_last_error.c_str(); }
 // delays from LDS instead of HBM when ipw * row fits).
 constexpr int32_t kDelayStageWords = 2048;
 // Workgroups (4 waves each) per CU the automatic FIFO sizing keeps LDS from limiting (the
-// spill-free kernels of degree bounds 3-4 run 6 waves per SIMD; deeper queues go through the
-// spill fix-up).
+// spill-free kernels of degree bounds 3-4 run 6 waves per SIMD; deeper queues spill to HBM).
 constexpr int32_t kTargetBlocks = 6;
 // Batches of at least this many instances replay through a length-ordered slot map (a few
 // thousand waves: the grouping pays for its one host sort and 4 B per instance of HBM).
@@ -277,22 +276,27 @@ struct cl_sim {
   DevBuf<int32_t> d_snap_tick;
   DevBuf<uint32_t> d_ovf;
   DevBuf<uint32_t> d_ovh;
-  // Spill fix-up of fresh full runs (cl_kernels.hip launch_exec_fixup): the spill-free main
-  // pass lists the instances its LDS rings could not hold; the fix-up re-runs them with the
-  // HBM spill rings.  Two worklist counters alternate: a pair's fix-up zeroes the other one.
-  DevBuf<uint32_t> d_fix;      // [n_inst] worklist
-  DevBuf<uint32_t> d_fixc;     // [2] counters
-  int32_t fix_par = 0;         // counter the next main pass appends to
-  int32_t fix_last = -1;       // counter the last fix-up pair used (-1: none)
-  // Replays grouped by length: after a fresh full run of ops [0, map_ops) the host orders the
-  // instances by their final tick (d_map: slot -> instance) so the 64 / N instances sharing a
+  // Replay plan (build_plan), from the first fresh full run of ops [0, plan_ops) with these
+  // delays and layout -- the probe, run on the spill-capable kernel with per-instance spill
+  // flags.  Its replays (cl_rerun: the same program and delays, hence the same queues and
+  // final ticks) launch through a slot map d_map: instances grouped by their final tick so the
+  // 64 / N instances sharing a wave end their drains together, and the instances that spilled
+  // last; slots [0, split_slot) then run the spill-free kernel (6 waves per SIMD at degree
+  // bounds 3-4) and the rest the spill-capable one, concurrently on stream2.  Results are per
+  // instance and identical on either kernel.
+  DevBuf<uint8_t> d_spill_inst;  // [n_inst] probe: 1 where a push spilled to HBM
+  int64_t plan_ops = -1;         // program length the plan holds for (-1: none)
+  int64_t plan_tried = -1;       // program length a probe last ran for
+  bool probe = false;            // the last launch was a probe (plan built at the next sync)
+  int64_t probe_ops = 0;
+  bool probe_flags = false;      // the probe recorded spill flags
+  bool plan_map = false, plan_nospill = false;
+  int64_t plan_split = 0, plan_spilled = 0;
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // wave end their drains together; replays of the same program and delays launch through
   // the map (results are per instance, unchanged).  -1: no map.
   DevBuf<int32_t> d_map;
-  int64_t map_ops = -1;
-  bool map_probe = false;       // the last launch was a fresh unmapped full run
-  int64_t map_probe_ops = 0;
-  int64_t map_tried = -1;       // the program length a map was last built (or rejected) for
   DevBuf<int32_t> d_hist;
   DevBuf<unsigned long long> d_sums;
   // device event trace (cl_trace_enable): instances [trace_lo, trace_lo + trace_n)
@@ -321,7 +325,7 @@ struct cl_sim {
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
-      d_ovh.release(); d_fix.release(); d_fixc.release(); d_map.release(); d_hist.release(); d_sums.release();
+      d_ovh.release(); d_spill_inst.release(); d_map.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       d_pk_tok.release(); d_pk_done.release(); d_pk_msg.release(); d_pk_cnt.release(); d_pk_bsum.release();
       d_pk_off.release(); d_rec2.release();
@@ -331,6 +335,9 @@ struct cl_sim {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
       }
+      if (stream2) (void)hipStreamDestroy(stream2);
+      if (ev_fork) (void)hipEventDestroy(ev_fork);
+      if (ev_join) (void)hipEventDestroy(ev_join);
       (void)hipStreamDestroy(stream);
     }
   }
@@ -459,7 +466,7 @@ struct cl_sim {
       if (rc) return rc;
       HIP_TRY(hipMemcpy(d_sched.p, sched.data(), sched.size(), hipMemcpyHostToDevice));
       dev_draws = D;  // longer rows of the same streams: saved draw cursors stay valid
-      map_ops = map_tried = -1;
+      plan_ops = plan_tried = -1;
       dev_row = D;
       return CL_OK;
     }
@@ -474,7 +481,7 @@ struct cl_sim {
     HIP_TRY(hipMemcpy(d_sched.p, padded.data(), padded.size(), hipMemcpyHostToDevice));
     dev_draws = user_draws;
     dev_row = row;
-    map_ops = map_tried = -1;
+    plan_ops = plan_tried = -1;
     return CL_OK;
   }
 
@@ -531,16 +538,8 @@ struct cl_sim {
     const size_t ov = lay.ocap_log2 >= 0 ? ((size_t)C << lay.ocap_log2) * stride : 1;
     if ((rc = d_ovf.ensure(ov))) return rc;
     if ((rc = d_ovh.ensure(lay.ocap_log2 >= 0 ? (size_t)std::max(C, 1) * stride : 1))) return rc;
-    if (lay.ocap_log2 >= 0) {
-      if ((rc = d_fix.ensure((size_t)n_inst))) return rc;
-      if (!d_fixc.p) {
-        if ((rc = d_fixc.ensure(2))) return rc;
-        HIP_TRY(hipMemset(d_fixc.p, 0, 2 * sizeof(uint32_t)));
-        fix_par = 0;
-        fix_last = -1;
-      }
-    }
-    map_ops = map_tried = -1;
+    if (lay.ocap_log2 >= 0 && (rc = d_spill_inst.ensure((size_t)n_inst))) return rc;
+    plan_ops = plan_tried = -1;
     need_fresh = true;
     return CL_OK;
   }
@@ -662,17 +661,27 @@ struct cl_sim {
     // cl_exec_kernel prologue -- no fill launch before every replay)
     ExecParams p = exec_params(begin, started_before);
     p.save_state = save_state ? 1 : 0;
-    // a fresh full run with spill rings in the layout: spill-free main pass + fix-up (the
-    // launcher decides whether its kernels are specialized for the layout)
-    if (begin == 0 && trace_n == 0 && lay.ocap_log2 >= 0) {
-      p.fix_list = d_fix.p;
-      p.fix_count = d_fixc.p + fix_par;
-      p.fix_clear = d_fixc.p + (fix_par ^ 1);
-      p.fix_blocks = fix_blocks();
+    // replays of a planned program (build_plan): slot map, spill-free or split launches
+    const bool planned = begin == 0 && trace_n == 0 && plan_ops == (int64_t)ops.size();
+    if (planned) {
+      p.inst_map = plan_map ? d_map.p : nullptr;
+      p.nospill = plan_nospill ? 1 : 0;
+      p.split_slot = plan_split;
     }
-    p.inst_map = begin == 0 && map_ops == (int64_t)ops.size() ? d_map.p : nullptr;
-    map_probe = begin == 0 && !p.inst_map && n_inst >= kMapMinInstances && map_tried != (int64_t)ops.size();
-    map_probe_ops = (int64_t)ops.size();
+    // the first fresh full run of a program is the probe: per-instance spill flags (cleared
+    // once per program, not per replay) and final ticks
+    probe = begin == 0 && trace_n == 0 && !planned && plan_tried != (int64_t)ops.size();
+    probe_ops = (int64_t)ops.size();
+    probe_flags = probe && lay.ocap_log2 >= 0;
+    if (probe_flags) {
+      HIP_TRY(hipMemsetAsync(d_spill_inst.p, 0, (size_t)n_inst, stream));
+      p.spill_flag = d_spill_inst.p;
+    }
+    if (p.split_slot > 0 && !stream2) {
+      HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
     if (ev_used == 256 && (rc = fold_events())) return rc;
     if (ev_used == ev_pool.size()) {
       std::pair<hipEvent_t, hipEvent_t> pr;
@@ -684,15 +693,8 @@ struct cl_sim {
     // the dispatch records both events (the kernel's own start/end timestamps): two
     // hipEventRecord packets around it cost 0.7 us more per launch (C2 0.1816 -> 0.1809 ms per
     // step) and bracketed ~1 us of packet processing into the kernel time
-    int32_t fixed = 0;
-    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p, ExecLaunch{stream, pr.first, pr.second, &fixed});
+    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p, ExecLaunch{stream, pr.first, pr.second, stream2, ev_fork, ev_join});
     if (e != 0) return set_err(CL_E_DEVICE, "exec kernel launch failed: %s", hipGetErrorString((hipError_t)e));
-    if (fixed) {  // this pair used counter fix_par and zeroed the other for the next pair
-      fix_last = fix_par;
-      fix_par ^= 1;
-    } else {
-      fix_last = -1;
-    }
     ev0 = pr.first;
     ev1 = pr.second;
     timed = true;
@@ -703,71 +705,81 @@ struct cl_sim {
     return CL_OK;
   }
 
-  // The launcher's specialized kernels (and so the spill fix-up) serve this layout: unrolled
+  // The launcher's specialized kernels (and so split replays) serve this layout: unrolled
   // degree bound, staged delays, 2 / 4 / 8 LDS ring slots (cl_kernels.hip launch_exec_d).
   bool specialized() const {
     const int32_t d = std::max(std::max(max_out, max_in), 1);
     return degree_bound(d) <= kUnrollMaxD && lay.x_delay > 0 && lay.cap_log2 >= 1 && lay.cap_log2 <= 3;
   }
 
-  // Fix-up grid: persistent waves over the worklist, sized to the resident capacity of the
-  // fix-up kernel (3 waves per SIMD: it keeps its registers; LDS per CU)
-  int32_t fix_blocks() const {
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-    const int64_t by_lds = (int64_t)kMaxLdsBytes / std::max<int64_t>(1, (int64_t)lay.wave_words * 4 * lay.wpb);
-    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(3, by_lds));
-    const int64_t need = ((n_inst + lay.ipw - 1) / lay.ipw + lay.wpb - 1) / lay.wpb;
-    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(need, per_cu * cus));
-  }
-
   int sync() {
     if (!dev_ready) return CL_OK;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamSynchronize(stream));
-    if (map_probe) {
-      map_probe = false;
-      int rc = build_map();
+    if (probe) {
+      probe = false;
+      int rc = build_plan();
       if (rc) return rc;
     }
     return CL_OK;
   }
 
-  // Slot -> instance order of the last fresh full run's final ticks (counting sort, stable).
-  int build_map() {
-    map_tried = map_probe_ops;
+  // Sum over waves of the longest instance (wave-ticks) of a slot order.
+  int64_t wave_ticks(const std::vector<int32_t>& t, const std::vector<int32_t>& order, int64_t lo, int64_t hi) const {
+    const int64_t ipw = std::max(lay.ipw, 1);
+    int64_t sum = 0;
+    for (int64_t w = lo; w < hi; w += ipw) {
+      int32_t m = 0;
+      for (int64_t k = w; k < std::min<int64_t>(w + ipw, hi); ++k) m = std::max(m, t[(size_t)order[(size_t)k]]);
+      sum += m;
+    }
+    return sum;
+  }
+
+  // The replay plan from the probe's final ticks and spill flags (see d_spill_inst).
+  int build_plan() {
+    plan_tried = probe_ops;
+    plan_map = plan_nospill = false;
+    plan_split = plan_spilled = 0;
     std::vector<int32_t> t((size_t)n_inst);
     HIP_TRY(hipMemcpy2D(t.data(), sizeof(int32_t), d_regs.p + R_TIME, R_NUM * sizeof(int32_t), sizeof(int32_t), t.size(),
                         hipMemcpyDeviceToHost));
+    std::vector<uint8_t> sp((size_t)n_inst, 0);
+    if (probe_flags) HIP_TRY(hipMemcpy(sp.data(), d_spill_inst.p, sp.size(), hipMemcpyDeviceToHost));
+    std::vector<int32_t> clean, spilled, ident((size_t)n_inst);
+    for (int64_t i = 0; i < n_inst; ++i) {
+      ident[(size_t)i] = (int32_t)i;
+      (sp[(size_t)i] ? spilled : clean).push_back((int32_t)i);
+    }
+    plan_spilled = (int64_t)spilled.size();
+    plan_nospill = spilled.empty();
+    // length order of the clean instances: one global counting sort by final tick (sorting
+    // within windows of 64 waves instead, to keep each window's scattered per-instance stores
+    // close in time, measured C3 2.71 -> 2.96 ms: the global order is kept)
     int32_t mx = 0;
     for (int32_t x : t) mx = std::max(mx, std::max(x, 0));
-    // one global counting sort by final tick (sorting within windows of 64 waves instead, to
-    // keep each window's scattered per-instance stores close in time, measured C3 2.71 ->
-    // 2.96 ms: the global order is kept)
-    const int64_t ipw = std::max(lay.ipw, 1);
     std::vector<int64_t> start((size_t)mx + 2, 0);
-    for (int32_t x : t) start[(size_t)std::max(x, 0) + 1]++;
+    for (int32_t i : clean) start[(size_t)std::max(t[(size_t)i], 0) + 1]++;
     for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
-    std::vector<int32_t> order((size_t)n_inst);
-    for (int64_t i = 0; i < n_inst; ++i) order[(size_t)start[(size_t)std::max(t[(size_t)i], 0)]++] = (int32_t)i;
-    // worth it only when it removes enough wave-ticks to pay for the scattered stores: sum
-    // over waves of the longest instance, in launch order vs in length order (C3: 43.9 -> 39.5
-    // ticks per wave, kept; C2: 55.8 -> 52.8, measured slower mapped, left in launch order)
-    int64_t as_is = 0, sorted = 0;
-    for (int64_t w = 0; w < n_inst; w += ipw) {
-      int32_t a = 0, b = 0;
-      for (int64_t k = w; k < std::min<int64_t>(w + ipw, n_inst); ++k) {
-        a = std::max(a, t[(size_t)k]);
-        b = std::max(b, t[(size_t)order[(size_t)k]]);
-      }
-      as_is += a;
-      sorted += b;
+    std::vector<int32_t> by_len(clean.size());
+    for (int32_t i : clean) by_len[(size_t)start[(size_t)std::max(t[(size_t)i], 0)]++] = i;
+    // worth it only when it removes enough wave-ticks to pay for the scattered stores (C3:
+    // 43.9 -> 39.5 ticks per wave, kept; C2: 55.8 -> 52.8, measured slower mapped)
+    const int64_t nc = (int64_t)clean.size();
+    const bool sort = n_inst >= kMapMinInstances && wave_ticks(t, by_len, 0, nc) * 100 <= wave_ticks(t, clean, 0, nc) * 92;
+    std::vector<int32_t> order = sort ? by_len : clean;
+    order.insert(order.end(), spilled.begin(), spilled.end());
+    const int64_t ipw = std::max(lay.ipw, 1);
+    // split replays: the clean instances' whole waves on the spill-free kernel (a wave that
+    // holds a spilling instance runs spill-capable), when the launcher's kernels can split
+    if (!spilled.empty() && specialized()) plan_split = nc / ipw * ipw;
+    plan_map = sort || plan_split > 0;
+    if (plan_map) {
+      int rc = d_map.ensure(order.size());
+      if (rc) return rc;
+      HIP_TRY(hipMemcpy(d_map.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     }
-    if (sorted * 100 > as_is * 92) return CL_OK;  // under 8 % fewer wave-ticks: keep launch order
-    int rc = d_map.ensure(order.size());
-    if (rc) return rc;
-    HIP_TRY(hipMemcpy(d_map.p, order.data(), order.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    map_ops = map_probe_ops;
+    plan_ops = probe_ops;
     return CL_OK;
   }
 
@@ -1056,7 +1068,7 @@ int cl_set_limits(cl_sim* sim, int32_t fifo_lds_slots, int64_t max_drain_ticks) 
 
 int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
   SIM_CHECK(sim);
-  sim->map_ops = sim->map_tried = -1;
+  sim->plan_ops = sim->plan_tried = -1;
   sim->go_seeds = true;
   sim->seed_base = seed_base;
   sim->dev_draws = -1;
@@ -1066,7 +1078,7 @@ int cl_set_delay_go_seeds(cl_sim* sim, int64_t seed_base) {
 
 int cl_set_delay_schedule(cl_sim* sim, const uint8_t* delays, int64_t draws_per_instance) {
   SIM_CHECK(sim);
-  sim->map_ops = sim->map_tried = -1;
+  sim->plan_ops = sim->plan_tried = -1;
   if (!delays || draws_per_instance <= 0) return set_err(CL_E_INVALID, "empty schedule");
   const size_t n = (size_t)(draws_per_instance * sim->n_inst);
   for (size_t i = 0; i < n; ++i)
@@ -1198,20 +1210,18 @@ int cl_replay_spill_free(cl_sim* sim, int32_t* on) {
   if (!on) return set_err(CL_E_INVALID, "null output");
   int rc = sim->sync();
   if (rc) return rc;
-  *on = sim->lay.ocap_log2 < 0 || sim->specialized() ? 1 : 0;
+  *on = sim->lay.ocap_log2 < 0 || (sim->plan_ops == (int64_t)sim->ops.size() && sim->plan_nospill) ? 1 : 0;
   return CL_OK;
 }
 
-int cl_fixup_instances(cl_sim* sim, int64_t* n) {
+int cl_replay_split(cl_sim* sim, int64_t* spill_instances, int64_t* split_slot) {
   SIM_CHECK(sim);
-  if (!n) return set_err(CL_E_INVALID, "null output");
-  int rc = sim->sync();
+  if (!spill_instances || !split_slot) return set_err(CL_E_INVALID, "null output");
+  int rc = sim->sync();  // (a pending probe is evaluated here)
   if (rc) return rc;
-  *n = 0;
-  if (sim->fix_last < 0) return CL_OK;
-  uint32_t c = 0;  // (zeroed only by the next pair's fix-up)
-  HIP_TRY(hipMemcpy(&c, sim->d_fixc.p + sim->fix_last, sizeof c, hipMemcpyDeviceToHost));
-  *n = c;
+  const bool planned = sim->plan_ops == (int64_t)sim->ops.size();
+  *spill_instances = planned ? sim->plan_spilled : -1;
+  *split_slot = planned ? sim->plan_split : 0;
   return CL_OK;
 }
 
@@ -1220,7 +1230,7 @@ int cl_replay_mapped(cl_sim* sim, int32_t* on) {
   if (!on) return set_err(CL_E_INVALID, "null output");
   int rc = sim->sync();  // (a pending map probe is evaluated here)
   if (rc) return rc;
-  *on = sim->map_ops == (int64_t)sim->ops.size() ? 1 : 0;
+  *on = sim->plan_ops == (int64_t)sim->ops.size() && sim->plan_map ? 1 : 0;
   return CL_OK;
 }
 

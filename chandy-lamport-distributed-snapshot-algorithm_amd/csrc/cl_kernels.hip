@@ -218,6 +218,7 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
     if (cnt == cap) *hp = 0u;
     else h = *hp;
     x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.stride + x.inst] = e;
+    if (x.p.spill_flag) x.p.spill_flag[x.inst] = 1;  // (the replay plan: this instance needs the rings)
   }
   CHW(ko) = (uint16_t)(chw + kCountOne);
   ln.push++;
@@ -562,23 +563,20 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
 #ifndef CLSNAP_W4
 #define CLSNAP_W4 5  // D = 3, 4 with HBM spill rings: 5 waves/SIMD, DESIGN.md §9
 #endif
-#ifndef CLSNAP_FIXUP
-#define CLSNAP_FIXUP 1  // A/B knob: 0 runs fresh full runs with spill rings on the spill-capable kernel
+#ifndef CLSNAP_SPLIT
+#define CLSNAP_SPLIT 1  // A/B knob: 0 replays a batch with spilling instances wholly on the spill-capable kernel
 #endif
 #ifndef CLSNAP_W4NS
 #define CLSNAP_W4NS 6  // D = 3, 4 spill-free (the main pass of BASELINE config 3): 6 waves/SIMD
 #endif
-// The spill fix-up runs few waves, each latency-bound through a whole instance: it takes
-// registers over occupancy (2 waves per SIMD: no scratch spills in the tick loop).
-constexpr int waves_for(int D, bool spill, bool fixup) {
-  return fixup ? 2
-         : D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1)
+constexpr int waves_for(int D, bool spill) {
+  return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1)
          : (D == 3 || D == 4) ? (spill ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : CLSNAP_W4NS) : 1;
 }
 
 // The whole event program for the instances of one wave (slots wave * ipw .. + ipw - 1 of
 // the launch; n_slots slots in all).  Every lane of the wave must call it.
-template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED, bool FIXUP>
+template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED>
 __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay, uint32_t wave, uint32_t n_slots,
                                           const int32_t* imap, lds_u32* X, const uint32_t* __restrict__ topo,
                                           const Op* __restrict__ ops, const uint8_t* __restrict__ sched) {
@@ -587,10 +585,10 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   const int32_t seg = lane / N;
   const int32_t v = lane - seg * N;
   // slot = position in the launch; inst = the instance it runs (imap: replays grouped by
-  // length so a wave's segments finish together, or the spill fix-up's worklist, cl_host.cpp)
+  // length, spilling instances last, so a wave's segments finish together; cl_host.cpp)
   // (MAPPED: specialized kernels launch with a map, the others without; the generic CAP = 0
   // kernel checks at run time)
-  const uint32_t slot = wave * (uint32_t)lay.ipw + seg;
+  const uint32_t slot = p.slot_base + wave * (uint32_t)lay.ipw + seg;
   const bool valid = seg < lay.ipw && slot < n_slots;
   const uint32_t inst = ((CAP > 0 || imap) && MAPPED && valid) ? (uint32_t)imap[slot] : slot;
   const uint32_t ii = valid ? inst : 0u;  // safe index for lanes without an instance
@@ -601,7 +599,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   // Stage the wave's delay rows (ipw contiguous rows of sched_row bytes) in LDS when they fit.
   const lds_u8* lrow = STAGED ? (const lds_u8*)(X + lay.x_delay) + (size_t)seg * p.sched_row : nullptr;
   if constexpr (STAGED) {
-    const uint32_t first = wave * (uint32_t)lay.ipw;
+    const uint32_t first = p.slot_base + wave * (uint32_t)lay.ipw;
     const uint32_t nrow = min((uint32_t)lay.ipw, n_slots - min(first, n_slots));
     const uint32_t rw4 = (uint32_t)(p.sched_row / 4);
     if (!MAPPED || (CAP == 0 && !imap)) {  // consecutive instances: one contiguous copy
@@ -789,11 +787,6 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
     r[R_POP_MK] = (int32_t)acc[2];
     r[R_PUSH] = (int32_t)acc[3];
     r[R_INFLIGHT_TOK] = (int32_t)acc[4];
-    // spill-free main pass: an instance frozen by a full LDS ring (or a queue past 255) is
-    // re-run from the initial state by the spill fix-up launch, which either spills it to
-    // HBM or freezes it with the same status at the same push
-    if constexpr (!SPILL && !FIXUP)
-      if (p.fix_list && ln.status == ST_FIFO_OVERFLOW) p.fix_list[atomicAdd(p.fix_count, 1u)] = ii;
   }
   if (!p.save_state) return;
   uint32_t* S = p.state + ii;
@@ -819,12 +812,9 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
 // CAP > 0: the layout's private column is ColumnC<D, CAP> (compile-time offsets: register
 // pressure of the D = 3 kernel 95 VGPRs + 58 SGPR spills -> ~80 VGPRs, no spills); SPILL false
 // compiles out the HBM spill rings.  CAP = 0 reads every offset from the runtime layout (any
-// D, any ring size).  FIXUP: the spill fix-up -- persistent waves over the worklist the
-// spill-free main pass filled (p.fix_list, *p.fix_count entries); it also zeroes the other
-// counter of the pair (p.fix_clear) for the next main pass.  Every wave exits once the list
-// is exhausted.
-template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED, bool FIXUP = false>
-__global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D, SPILL, FIXUP)) void cl_exec_kernel(
+// D, any ring size).  The grid covers slots [p.slot_base, p.n_inst).
+template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED>
+__global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D, SPILL)) void cl_exec_kernel(
     ExecParams p, const uint32_t* __restrict__ topo, const Op* __restrict__ ops, const uint8_t* __restrict__ sched) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   Layout lay_ = p.lay;
@@ -846,21 +836,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D, SPILL, FIXUP))
   const Layout& lay = lay_;
   const int32_t wib = threadIdx.x / kWave;
   lds_u32* X = (lds_u32*)(lds + (size_t)wib * lay.wave_words);
-  if constexpr (FIXUP) {
-    static_assert(MAPPED && SPILL, "the fix-up re-runs listed instances with spill rings");
-    const uint32_t n = *p.fix_count;
-    if (blockIdx.x == 0 && threadIdx.x == 0) *p.fix_clear = 0u;
-    const uint32_t nw = (n + (uint32_t)lay.ipw - 1) / (uint32_t)lay.ipw;
-    for (uint32_t w = blockIdx.x * (uint32_t)p.lay.wpb + wib; w < nw; w += gridDim.x * (uint32_t)p.lay.wpb) {
-      wave_sync();
-      exec_wave<D, STAGED, TRACE, CAP, SPILL, MAPPED, FIXUP>(p, lay, w, n, reinterpret_cast<const int32_t*>(p.fix_list),
-                                                             X, topo, ops, sched);
-    }
-  } else {
-    exec_wave<D, STAGED, TRACE, CAP, SPILL, MAPPED, FIXUP>(p, lay, blockIdx.x * (uint32_t)p.lay.wpb + wib,
-                                                           (uint32_t)p.n_inst, MAPPED ? p.inst_map : nullptr, X, topo,
-                                                           ops, sched);
-  }
+  exec_wave<D, STAGED, TRACE, CAP, SPILL, MAPPED>(p, lay, blockIdx.x * (uint32_t)p.lay.wpb + wib, (uint32_t)p.n_inst,
+                                                  MAPPED ? p.inst_map : nullptr, X, topo, ops, sched);
 }
 
 #undef PW
@@ -1050,42 +1027,53 @@ __global__ __launch_bounds__(256) void cl_pack_fill(PackParams p) {
 
 }  // namespace
 
-template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true, bool FIXUP = false>
-int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
+template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true>
+int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L,
+                   void* stream = nullptr) {
   const int32_t wpb = p.lay.wpb;
   const size_t lds = (size_t)p.lay.wave_words * wpb * sizeof(uint32_t);
-  auto* k = cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED, FIXUP>;
+  auto* k = cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
-  const int64_t waves = (p.n_inst + p.lay.ipw - 1) / p.lay.ipw;
-  const unsigned blocks = FIXUP ? (unsigned)p.fix_blocks : (unsigned)((waves + wpb - 1) / wpb);
-  hipExtLaunchKernelGGL(k, dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)L.stream, (hipEvent_t)L.ev_start,
-                        (hipEvent_t)L.ev_stop, 0u, p, topo, ops, sched);
+  const int64_t waves = (p.n_inst - p.slot_base + p.lay.ipw - 1) / p.lay.ipw;
+  const unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
+  if (blocks == 0) return 0;
+  hipExtLaunchKernelGGL(k, dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)(stream ? stream : L.stream),
+                        (hipEvent_t)(stream ? nullptr : L.ev_start), (hipEvent_t)(stream ? nullptr : L.ev_stop), 0u, p,
+                        topo, ops, sched);
   return (int)hipGetLastError();
 }
 
-// A fresh full run with the spill fix-up: the spill-free main pass (6 waves per SIMD for D =
-// 3, 4: smaller register and LDS footprint), then the spill-capable kernel over the instances
-// it froze.  The dispatches record the start (main) and stop (fix-up) events.
-template <int D, int CAP, bool MAPPED>
-int launch_exec_fixup(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched,
+// A replay split by the plan of its first run (cl_host.cpp build_plan): the slot map puts the
+// instances whose queues outgrew the LDS rings last; slots [0, split) run on the spill-free
+// kernel (6 waves per SIMD for D = 3, 4), slots [split, n) on the spill-capable one,
+// concurrently on a second stream (fork / join events).  The main dispatch records the start
+// event; the stop event is recorded after the join.
+template <int D, int CAP>
+int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched,
                       const ExecLaunch& L) {
-  ExecLaunch a = L, b = L;
-  a.ev_stop = nullptr;
-  b.ev_start = nullptr;
-  int e = launch_exec_ds<D, true, false, CAP, false, MAPPED>(p, topo, ops, sched, a);
+  hipStream_t s = (hipStream_t)L.stream, s2 = (hipStream_t)L.stream2;
+  hipError_t he;
+  if ((he = hipEventRecord((hipEvent_t)L.ev_fork, s)) || (he = hipStreamWaitEvent(s2, (hipEvent_t)L.ev_fork, 0)))
+    return (int)he;
+  ExecParams a = p, b = p;
+  a.n_inst = p.split_slot;
+  b.slot_base = (uint32_t)p.split_slot;
+  ExecLaunch la = L;
+  la.ev_stop = nullptr;
+  int e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la);
   if (e) return e;
-  if (L.fixup_launched) *L.fixup_launched = 1;
-  return launch_exec_ds<D, true, false, CAP, true, true, true>(p, topo, ops, sched, b);
+  if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, L, s2))) return e;
+  if ((he = hipEventRecord((hipEvent_t)L.ev_join, s2)) || (he = hipStreamWaitEvent(s, (hipEvent_t)L.ev_join, 0)))
+    return (int)he;
+  if (L.ev_stop && (he = hipEventRecord((hipEvent_t)L.ev_stop, s))) return (int)he;
+  return 0;
 }
 
 template <int D>
-int launch_exec_d(const ExecParams& pf, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
-  // (only the specialized spill-free main pass appends to the fix-up worklist)
-  ExecParams p = pf;
-  p.fix_list = nullptr;
+int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L) {
   // The trace build reads delays from HBM (one instantiation per D, debug runs only).
   if (p.trace_n > 0) return launch_exec_ds<D, false, true>(p, topo, ops, sched, L);
   if constexpr (unrolled(D)) {
@@ -1093,16 +1081,14 @@ int launch_exec_d(const ExecParams& pf, const uint32_t* topo, const Op* ops, con
     // specialized on the column layout, with or without HBM spill rings
     const bool ok = p.lay.od == D && p.lay.id == D;
     if (p.lay.x_delay > 0 && ok) {
-      // spill rings in the layout: a fresh full run takes the spill-free main pass and the
-      // fix-up; a resumed launch (state may hold spilled queues) the spill-capable kernel
-      const bool rings = p.lay.ocap_log2 >= 0;
-      const bool fix = CLSNAP_FIXUP && rings && pf.fix_list != nullptr;
-      if (fix) p.fix_list = pf.fix_list;
+      // spill rings in the layout: the spill-capable kernel, unless the replay plan knows the
+      // program never spills (p.nospill) or splits the batch (p.split_slot)
+      const bool rings = p.lay.ocap_log2 >= 0 && !p.nospill;
       const bool mp = p.inst_map != nullptr;
+      const bool split = CLSNAP_SPLIT && rings && mp && p.split_slot > 0 && p.split_slot < p.n_inst && L.stream2;
 #define CLSNAP_SPEC(C)                                                                              \
   case C:                                                                                           \
-    if (fix) return mp ? launch_exec_fixup<D, C, true>(p, topo, ops, sched, L)                  \
-                       : launch_exec_fixup<D, C, false>(p, topo, ops, sched, L);                \
+    if (split) return launch_exec_split<D, C>(p, topo, ops, sched, L);                          \
     if (rings) return mp ? launch_exec_ds<D, true, false, C, true, true>(p, topo, ops, sched, L)   \
                          : launch_exec_ds<D, true, false, C, true, false>(p, topo, ops, sched, L); \
     return mp ? launch_exec_ds<D, true, false, C, false, true>(p, topo, ops, sched, L)          \

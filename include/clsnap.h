@@ -143,17 +143,19 @@ int cl_last_kernel_ms(cl_sim* sim, double* ms);
 /* Sum of exec-kernel device times (HIP events around every launch) since the previous
  * call, and the number of launches; resets the accumulator. */
 int cl_kernel_time(cl_sim* sim, double* total_ms, int64_t* launches);
-/* 1 in *on when the next cl_rerun's main pass runs the spill-free kernel: the layout has no
- * HBM spill rings, or the engine's specialized kernels serve it -- a fresh full run then
- * runs every instance spill-free and re-runs only those whose LDS rings overflowed with the
- * spill rings (the spill fix-up; engine-internal, results are the same either way). */
+/* 1 in *on when the next cl_rerun runs wholly on the spill-free kernel: the layout has no HBM
+ * spill rings, or the first full run of the same program with the same delays and layout
+ * spilled nothing (engine-internal specialization; results are the same either way). */
 int cl_replay_spill_free(cl_sim* sim, int32_t* on);
-/* Instances the spill fix-up of the latest launch re-ran with HBM spill rings (0 when that
- * launch had no fix-up). */
-int cl_fixup_instances(cl_sim* sim, int64_t* n);
-/* 1 in *on when the next cl_rerun launches through the length-ordered slot map (instances
+/* The replay plan of the current program (from its first full run): instances whose queues
+ * outgrew the LDS rings (-1: no plan yet), and the slot from which replays run on the
+ * spill-capable kernel while the slots before it run spill-free, concurrently (0: no split).
+ * Engine-internal; results are the same either way. */
+int cl_replay_split(cl_sim* sim, int64_t* spill_instances, int64_t* split_slot);
+/* 1 in *on when the next cl_rerun launches through the replay plan's slot map (instances
  * grouped by the final tick of an earlier full run of the same program and delays, so the
- * instances sharing a wave finish together; engine-internal, results unchanged). */
+ * instances sharing a wave finish together, and those that spilled last; engine-internal,
+ * results unchanged). */
 int cl_replay_mapped(cl_sim* sim, int32_t* on);
 
 /* Test/benchmark aid (no reference counterpart): overwrite every result plane the exec

@@ -251,16 +251,16 @@ def test_rerun_equals_flush_and_oracle(cfg):
     top, events, n, slots = cfg
     sim = engine_run(top, events, n, fifo_lds_slots=slots)
     first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
-    # the main pass runs spill-free; instances whose LDS rings overflow are re-run with the
-    # HBM spill rings by the fix-up -- with two LDS slots, deep channels must need them
-    assert sim.spill_free_replays()
-    fixed = sim.fixup_instances()
+    # the replay plan of the flush (the probe): instances that spilled run last, on the
+    # spill-capable kernel, the rest spill-free -- with two LDS slots, deep channels spill
+    spilled, split = sim.replay_split()
+    assert 0 <= spilled <= n and (split == 0 or n - spilled - 64 < split <= n - spilled)
     if slots == 2:
-        assert fixed > 0
+        assert spilled > 0 and not sim.spill_free_replays()
+    if 0 < spilled < n - 64:
+        assert sim.mapped_replays() and split > 0
     if n == 131072 and slots is None:  # C3: instance lengths spread (13..50 ticks): mapped replays
         assert sim.mapped_replays()
-    if n == 65536:  # C2: too little spread to pay for the map
-        assert not sim.mapped_replays()
     _, st, ticks, cnt, hashes = oracle_batch(top, events, n, threads=16)
     want = batch_sums_from_oracle(st, cnt, hashes)
     # the poison reaches every plane the results are read from: without a rerun, nothing
@@ -272,7 +272,7 @@ def test_rerun_equals_flush_and_oracle(cfg):
         sim.poison_outputs()      # results below can only come from this rerun
         sim.rerun()
         sim.synchronize()
-        assert sim.fixup_instances() == fixed, f"rerun {r}: fix-up worklist"
+        assert sim.replay_split() == (spilled, split), f"rerun {r}: plan"
         status, times, sums = sim.status(), sim.time(), sim.checksums()
         assert np.array_equal(status, first[0]) and np.array_equal(status, st), f"rerun {r}: status"
         assert np.array_equal(times, first[1]), f"rerun {r}: times"
@@ -288,15 +288,15 @@ def test_rerun_equals_flush_and_oracle(cfg):
                          status=status, times=times)
 
 
-def test_spill_fixup_reruns_exactly_the_overflowing_instances():
-    """A fresh full run runs every instance spill-free; an instance whose push finds its
-    LDS ring full freezes with FIFO_OVERFLOW and is listed, and the fix-up launch re-runs
-    exactly the listed instances from the initial state with the HBM spill rings.  Two LDS
-    slots: A->B carries a send and two markers; with ticks between them the queue never
-    holds more than two packets, so nothing needs the fix-up -- until appended events queue
-    five tokens at once on A->B.  Every launch equals the oracle, incremental flushes
-    (spill-capable resumed launches) included, and the worklist counters alternate cleanly
-    across launches."""
+def test_replay_plan_spill_free_and_split():
+    """The first full run of a program is the probe: per-instance spill flags and final
+    ticks.  A program that never spills replays wholly on the spill-free kernel; one in which
+    some instances spill replays split -- the slot map puts the spilling instances last, the
+    clean whole waves run spill-free and the rest on the spill-capable kernel, concurrently
+    -- and appending events invalidates the plan until the next full run.  Every launch
+    equals the flush and the oracle; output planes are poisoned before every rerun."""
+    # A->B carries a send and two markers (depth bound 3 > 2 LDS slots: spill rings are
+    # provisioned), but the ticks between them keep at most one packet queued
     top = "3\nA 10\nB 10\nC 10\nA B\nB C\nC A\nB A\n"
     ev = "send A B 2\ntick 6\nsnapshot A\ntick 6\nsnapshot B\n"
     n = 512
@@ -304,41 +304,48 @@ def test_spill_fixup_reruns_exactly_the_overflowing_instances():
     sim.read_topology_text(top)
     sim.read_events_text(ev)
     sim.flush()
-    assert sim.spill_free_replays() and sim.fixup_instances() == 0
     first = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
+    assert sim.spill_free_replays() and sim.replay_split() == (0, 0)
     for i in range(0, n, 37):
         compare_instance(sim, i, oracle_run(top, ev, seed=O.REFERENCE_SEED + i), status=first[0], times=first[1])
     for _ in range(2):
         sim.poison_outputs()
         sim.rerun()
         sim.synchronize()
-        assert sim.fixup_instances() == 0
         assert np.array_equal(sim.status(), first[0]) and np.array_equal(sim.time(), first[1])
         assert np.array_equal(sim.checksums(), first[2])
     ev2 = "send A B 1\nsend A B 1\nsend A B 1\nsend A B 1\nsend A B 1\ntick 1\n"
     sim.read_events_text(ev2)
-    sim.flush()                   # (after reruns: a fresh full run) every instance overflows
-    assert sim.fixup_instances() == n
-    ev3 = "send B A 1\nsend A B 1\ntick 2\n"
-    sim.read_events_text(ev3)
-    sim.flush()                   # resumed launch: the spill-capable kernel, no fix-up
-    assert sim.fixup_instances() == 0
-    inc = (sim.status().copy(), sim.time().copy(), sim.checksums().copy())
-    for r in range(3):
-        sim.poison_outputs()
-        sim.rerun()               # fresh full run: every instance overflows two LDS slots
-        sim.synchronize()
-        assert sim.fixup_instances() == n, f"rerun {r}"
-        assert np.array_equal(sim.status(), inc[0]) and np.array_equal(sim.time(), inc[1])
-        assert np.array_equal(sim.checksums(), inc[2])
-    for i in range(0, n, 37):
-        o = O.OracleSim()
-        o.seed_go(O.REFERENCE_SEED + i)
-        assert o.read_topology_text(top) == 0
-        o.read_events_text(ev)
-        o.read_events_text(ev2)
-        o.read_events_text(ev3)
-        compare_instance(sim, i, o, status=inc[0], times=inc[1])
+    assert not sim.spill_free_replays() and sim.replay_split() == (-1, 0)   # (not run in full yet)
+    sim.rerun()                   # the new program's probe: every instance spills, no split
+    sim.synchronize()
+    assert sim.replay_split() == (n, 0)
+    ref = cl.ChandyLamportSim(n, fifo_lds_slots=2)  # the same two readEventsFile calls, one flush
+    ref.read_topology_text(top)
+    ref.read_events_text(ev)
+    ref.read_events_text(ev2)
+    ref.flush()
+    assert np.array_equal(sim.status(), ref.status()) and np.array_equal(sim.time(), ref.time())
+    assert np.array_equal(sim.checksums(), ref.checksums())
+    # random delays on 8nodes-concurrent with two LDS slots: some instances spill, most not
+    top3, ev3, n3 = "8nodes.top", "8nodes-concurrent-snapshots.events", 4096
+    sim3 = engine_run(top3, ev3, n3, fifo_lds_slots=2)
+    spilled, split = sim3.replay_split()
+    assert 0 < spilled < n3 - 64 and split > 0 and sim3.mapped_replays()
+    base = (sim3.status().copy(), sim3.time().copy(), sim3.checksums().copy())
+    for _ in range(2):
+        sim3.poison_outputs()
+        sim3.rerun()
+        sim3.synchronize()
+        assert np.array_equal(sim3.status(), base[0]) and np.array_equal(sim3.time(), base[1])
+        assert np.array_equal(sim3.checksums(), base[2])
+    _, st, ticks, cnt, hashes = oracle_batch(top3, ev3, n3)
+    want = batch_sums_from_oracle(st, cnt, hashes)
+    got = dict(zip(cl.SUM_NAMES, base[2].tolist()))
+    for k, v in want.items():
+        assert got[k] == v, k
+    for i in (0, 1, 77, 1234, n3 - 1):
+        compare_instance(sim3, i, oracle_run(top3, ev3, seed=O.REFERENCE_SEED + i), status=base[0], times=base[1])
 
 
 def test_headline_batch_2p20_matches_fixture():
