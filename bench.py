@@ -96,6 +96,7 @@ def parse_args():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-seed first-launch measurement")
+    ap.add_argument("--no-collect", action="store_true", help="skip the full-batch CollectSnapshot measurement")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo for rehearsals")
     ap.add_argument("--shared-device", action="store_true",
                     help="every rank on cuda:0 (multi-rank rehearsal on a one-GPU box)")
@@ -194,6 +195,7 @@ def main():
     # checksums of the LAST timed rerun (the timed path itself), all-reduced over ranks
     sums = sim.checksums()
     recorded_ok = sim.counters(only_ok=True)["recorded"]
+    collect = collect_all(sim, args) if not args.no_collect else None
     spilled, split = sim.replay_split()
     replay = {"slot_map": sim.mapped_replays(), "spill_free": sim.spill_free_replays(),
               "spilled_instances": spilled, "split_slot": split}
@@ -282,6 +284,7 @@ def main():
                        "snapshot_hash": tot["snapshot_hash"], "completed": tot["completed"],
                        "recorded": tot["recorded"]},
             "fresh_run": fresh,
+            "collect": collect,
             "replay": dict(replay, note="value is the replay rate: the timed steps re-run the same "
                                         "program and delays, launched through the slot map that the "
                                         "first run's final ticks give (DESIGN.md section 6); fresh_run is "
@@ -306,6 +309,30 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def collect_all(sim, args):
+    """CollectSnapshot (sim.go:134-173) of every snapshot over this rank's whole batch, packed
+    on the GPU (cl_collect_snapshot_packed) into host arrays: the reference's {tokenMap,
+    messages} for every instance.  Outside `value`.  Device ms = the packing kernels (HIP
+    events), wall ms = packing + the PCIe copies into pageable host memory, summed over the
+    snapshots (second pass: buffers already sized)."""
+    out = None
+    for _ in range(2):
+        dev, wall, msgs, nbytes = 0.0, 0.0, 0, 0
+        for sid in range(sim.num_snapshots):
+            t = time.perf_counter()
+            tok, done, off, msg = sim.collect_snapshot_packed(sid, out=out)
+            wall += time.perf_counter() - t
+            if out is None or msg.size > out[3].size:
+                out = (tok, np.zeros(done.size, dtype=np.int32), off, np.zeros(max(msg.size, 1024), dtype=np.int32))
+            dev += sim.collect_time()
+            msgs += int(msg.size)
+            nbytes += tok.nbytes + 4 * done.size + off.nbytes + 4 * msg.size
+    return {"snapshots": sim.num_snapshots, "instances": sim.n_instances, "messages": msgs,
+            "device_ms": dev, "wall_ms": wall * 1e3, "bytes_to_host": nbytes,
+            "note": "CollectSnapshot of every snapshot of the whole batch, packed on the GPU into one CSR "
+                    "over (instance, channel) per snapshot (cl_collect_snapshot_packed); not in value"}
 
 
 def fresh_run(cl, n, device, seed_base, top, events, args):

@@ -1,6 +1,6 @@
 """Turn a gpurun_out/pmc_<cfg> directory into committed profile summaries.
 
-usage: python tools/make_profiles.py <round> <cfg> [instances]
+usage: python tools/make_profiles.py <round> <cfg> [instances] [timed steps] [dispatches per step]
 writes profiles/<round>_<cfg>_kernel_stats.csv  (rocprofv3 --kernel-trace --stats)
        profiles/<round>_<cfg>_pmc.json          (per-dispatch PMC means, timed dispatches)
        profiles/traffic_<cfg>.json              (HBM bytes per launch for bench.py)
@@ -38,14 +38,22 @@ def main():
     os.makedirs(out, exist_ok=True)
     stats = os.path.join(src, "trace", "p_kernel_stats.csv")
     shutil.copy(stats, os.path.join(out, f"{rnd}_{cfg}_kernel_stats.csv"))
+    # one step = every exec-kernel dispatch of one rerun: split replays dispatch the spill-free
+    # and the spill-capable kernels concurrently.  Counters are summed over the timed steps'
+    # dispatches (the last steps * per_step of the pass) and divided by the steps; the active
+    # GPU cycles (GRBM_GUI_ACTIVE) of concurrent dispatches overlap, so the step's maximum.
+    steps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    per_step = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     summary = {}
     for name, per in per_dispatch(glob.glob(os.path.join(src, "pass*", "p_counter_collection.csv"))).items():
-        ds = sorted(per)
-        timed = ds[2:] if len(ds) > 2 else ds  # skip the first flush (writes state) and the warmup
-        summary[name] = sum(per[d] for d in timed) / len(timed)
+        ds = sorted(per)[-steps * per_step:]
+        groups = [ds[k:k + per_step] for k in range(0, len(ds), per_step)]
+        agg = max if name == "GRBM_GUI_ACTIVE" else sum
+        summary[name] = sum(agg(per[d] for d in g) for g in groups) / len(groups)
     with open(os.path.join(out, f"{rnd}_{cfg}_pmc.json"), "w") as f:
-        json.dump({"kernel": KERNEL, "config": cfg, "instances": inst,
-                   "note": "mean per timed dispatch; SQ_* cycle counters are quad-cycles",
+        json.dump({"kernel": KERNEL, "config": cfg, "instances": inst, "dispatches_per_step": per_step,
+                   "note": "per timed step (sum over its exec-kernel dispatches; GRBM_GUI_ACTIVE the "
+                           "max); SQ_* cycle counters are quad-cycles",
                    "counters": summary}, f, indent=1, sort_keys=True)
     if "FETCH_SIZE" in summary and "WRITE_SIZE" in summary:
         hbm = (2 * summary["FETCH_SIZE"] + summary["WRITE_SIZE"]) * 1024
