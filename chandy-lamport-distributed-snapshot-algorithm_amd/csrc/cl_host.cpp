@@ -55,6 +55,9 @@ constexpr int32_t kTargetBlocks = 6;
 // Batches of at least this many instances replay through a length-ordered slot map (a few
 // thousand waves: the grouping pays for its one host sort and 4 B per instance of HBM).
 constexpr int64_t kMapMinInstances = 4096;
+#ifndef CLSNAP_LPT
+#define CLSNAP_LPT 1  // slot map order: 1 longest instances first, 0 shortest first (A/B knob)
+#endif
 
 namespace {
 
@@ -763,6 +766,9 @@ struct cl_sim {
     for (size_t k = 1; k < start.size(); ++k) start[k] += start[k - 1];
     std::vector<int32_t> by_len(clean.size());
     for (int32_t i : clean) by_len[(size_t)start[(size_t)std::max(t[(size_t)i], 0)]++] = i;
+    // longest waves first (LPT): the dispatcher starts workgroups in slot order as resident
+    // ones retire, so the last to start are the shortest and the grid drains evenly
+    if (CLSNAP_LPT) std::reverse(by_len.begin(), by_len.end());
     // worth it only when it removes enough wave-ticks to pay for the scattered stores (C3:
     // 43.9 -> 39.5 ticks per wave, kept; C2: 55.8 -> 52.8, measured slower mapped)
     const int64_t nc = (int64_t)clean.size();
