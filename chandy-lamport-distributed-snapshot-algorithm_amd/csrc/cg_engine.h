@@ -197,7 +197,23 @@ struct GParams {
   int2* reports;         // [n] (s0, outdeg) broadcasts triggered by other devices' senders
   int32_t* trigv;        // [n] broadcasts triggered by owned senders this tick (draws)
   unsigned long long* rdraw;  // [n] first draw of broadcasts triggered by other devices' senders
+  // Device-resident exchange (cl_graph_part_dev_*): every exchange step moves
+  // fixed-capacity buckets of 16-B rows between device buffers (one bucket per peer rank:
+  // a header row {rows, 0, 0, 0} then bk_cap rows), so a tick needs no host round trip.
+  // bk_cap bounds every bucket exactly (from the topology: the senders of one rank with a
+  // channel into another's nodes).  Null bk_send: the host-staged exchange.
+  int32_t bk_world, bk_rank;
+  int32_t bk_span;     // node ranks per rank (owner(v) = v / bk_span)
+  int32_t bk_cap;      // rows per bucket after its header
+  int4* bk_send;       // [bk_world * (bk_cap + 1)] this rank's outgoing buckets
+  const int4* bk_recv; // [bk_world * (bk_cap + 1)] bucket q: what rank q sent here
+  uint32_t* bk_cnt;    // [bk_world] rows appended to each outgoing bucket
+  long long* tot_send;        // [4] this rank's tick totals: triggers, sends, status
+  const long long* tot_recv;  // [bk_world * 4] every rank's totals (all-gathered)
 };
+// Engine status of a device exchange bucket that overflowed its capacity (cannot happen with
+// the topology bound; a guard, never a wrong answer).
+constexpr int32_t kGStatusXchgOverflow = 7;
 
 // Launchers (cg_kernels.hip); return hipError_t as int.
 int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream);
@@ -224,6 +240,15 @@ int cg_launch_part_tally(const GParams& p, int32_t step, const int2* rep, int32_
 int cg_launch_part_bases(const GParams& p, int64_t trig_before, int64_t trig_all, int64_t send_before,
                          int64_t send_all, const int32_t* s0, int32_t n, unsigned long long* draw0, void* stream);
 int cg_launch_part_push(const GParams& p, int32_t t, int32_t step, const long long* replies, int32_t n, void* stream);
+// The same tick with the device-resident exchange (GParams bk_*): pick -> seal deliveries ->
+// [all-to-all] -> receive -> seal reports -> [all-to-all] -> tally -> [all-gather totals] ->
+// bases + replies -> [all-to-all] -> push.  No host round trip.
+int cg_launch_part_dev_seal(const GParams& p, void* stream);
+int cg_launch_part_dev_pick(const GParams& p, int32_t t, void* stream);
+int cg_launch_part_dev_receive(const GParams& p, int32_t t, void* stream);
+int cg_launch_part_dev_tally(const GParams& p, int32_t step, void* stream);
+int cg_launch_part_dev_bases(const GParams& p, void* stream);
+int cg_launch_part_dev_push(const GParams& p, int32_t t, int32_t step, void* stream);
 // Recorded copies on channels still recording at the end (out[0] += ...).
 int cg_launch_finish(const GParams& p, int32_t n_sids, unsigned long long* out, void* stream);
 // Batch checks (out zeroed by the caller, 3 + n_sids entries): out[0] final node tokens,

@@ -147,7 +147,8 @@ struct cl_graph {
   bool hang = false;
   bool state_valid = false;
   bool dev_ready = false;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // every launch and copy (cl_graph_set_stream may replace it)
+  hipStream_t own_stream = nullptr;  // the engine's own non-blocking stream
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   size_t ev_used = 0;
   double run_ms = 0;
@@ -193,6 +194,10 @@ struct cl_graph {
   GBuf<unsigned long long> d_rdraw, d_draw0;
   GBuf<long long> d_replies;
   GBuf<GOp> d_pop;
+  // device-resident exchange (cl_graph_part_dev_bind): caller-owned buckets and totals
+  int32_t bk_world = 0, bk_rank = 0, bk_span = 0, bk_cap = 0;
+  void *bk_send = nullptr, *bk_recv = nullptr, *tot_send = nullptr, *tot_recv = nullptr;
+  GBuf<uint32_t> d_bk_cnt;
 
   ~cl_graph() {
     if (!dev_ready) return;
@@ -208,14 +213,15 @@ struct cl_graph {
     d_trace.release(); d_trace_cnt.release();
     d_outbox.release(); d_inbox.release(); d_out_n.release(); d_rmlist.release(); d_reports.release();
     d_rep_in.release(); d_trigv.release(); d_s0.release(); d_rdraw.release(); d_draw0.release();
-    d_replies.release(); d_pop.release();
+    d_replies.release(); d_pop.release(); d_bk_cnt.release();
     for (auto& ev : ev_pool) {
       (void)hipEventDestroy(ev.first);
       (void)hipEventDestroy(ev.second);
     }
     for (auto& e : ph_ev)
       if (e) (void)hipEventDestroy(e);
-    (void)hipStreamDestroy(stream);
+    (void)hipStreamSynchronize(own_stream);
+    (void)hipStreamDestroy(own_stream);
   }
 
   // ---- topology --------------------------------------------------------------
@@ -408,6 +414,7 @@ struct cl_graph {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
       return gerr(CL_E_DEVICE, "device %d is %s, the engine is built for gfx950", device, prop.gcnArchName);
     GHIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    own_stream = stream;
     dev_ready = true;
     int rc;
     std::vector<int2> route((size_t)e);
@@ -542,6 +549,15 @@ struct cl_graph {
     p.reports = d_reports.p;
     p.trigv = d_trigv.p;
     p.rdraw = d_rdraw.p;
+    p.bk_world = bk_world;
+    p.bk_rank = bk_rank;
+    p.bk_span = bk_span;
+    p.bk_cap = bk_cap;
+    p.bk_send = (int4*)bk_send;
+    p.bk_recv = (const int4*)bk_recv;
+    p.bk_cnt = d_bk_cnt.p;
+    p.tot_send = (long long*)tot_send;
+    p.tot_recv = (const long long*)tot_recv;
   }
 
   int upload_ops() {
@@ -1629,6 +1645,85 @@ int cl_graph_part_push(cl_graph* g, int32_t step, const int64_t* replies, int64_
   if ((rc = g->k_err(cg_launch_part_push(g->P, (int32_t)g->time, step, g->d_replies.p, (int32_t)n, g->stream)))) return rc;
   GHIP(hipStreamSynchronize(g->stream));  // (the staged rows must outlive the launch)
   return CL_OK;
+}
+
+// ---- partitioned mode, device-resident exchange (clgraph.h cl_graph_part_dev_*) ----------
+int cl_graph_set_stream(cl_graph* g, void* stream) {
+  G_CHECK(g);
+  int rc = g->ensure_device();
+  if (rc) return rc;
+  GHIP(hipSetDevice(g->device));
+  GHIP(hipStreamSynchronize(g->stream));
+  g->stream = stream ? (hipStream_t)stream : g->own_stream;
+  return CL_OK;
+}
+
+#define G_DEV(g)                                                                                  \
+  do {                                                                                            \
+    G_CHECK(g);                                                                                   \
+    G_PART(g);                                                                                    \
+    if (!(g)->bk_send) return gerr(CL_E_STATE, "no device exchange buffers (cl_graph_part_dev_bind)"); \
+  } while (0)
+
+int cl_graph_part_dev_bind(cl_graph* g, int32_t world, int32_t rank, int32_t span, int64_t cap, void* send,
+                           void* recv, void* tot_send, void* tot_recv) {
+  G_CHECK(g);
+  G_PART(g);
+  if (world < 1 || rank < 0 || rank >= world || span <= 0 || span % kGThreads)
+    return gerr(CL_E_INVALID, "rank %d of %d, span %d (a positive multiple of %d)", rank, world, span, kGThreads);
+  if (g->part_lo != rank * span || g->part_hi != std::min<int64_t>((int64_t)(rank + 1) * span, g->n))
+    return gerr(CL_E_INVALID, "rank %d x span %d is not this device's range [%d, %d)", rank, span, g->part_lo,
+                g->part_hi);
+  if ((int64_t)world * span < g->n) return gerr(CL_E_INVALID, "%d ranks x %d nodes do not cover %d", world, span, g->n);
+  if (cap < 1 || cap > g->n) return gerr(CL_E_INVALID, "bucket capacity %lld", (long long)cap);
+  if (!send || !recv || !tot_send || !tot_recv) return gerr(CL_E_INVALID, "null exchange buffer");
+  GHIP(hipSetDevice(g->device));
+  int rc = g->d_bk_cnt.ensure((size_t)world);
+  if (rc) return rc;
+  GHIP(hipMemsetAsync(g->d_bk_cnt.p, 0, (size_t)world * sizeof(uint32_t), g->stream));
+  GHIP(hipStreamSynchronize(g->stream));
+  g->bk_world = world;
+  g->bk_rank = rank;
+  g->bk_span = span;
+  g->bk_cap = (int32_t)cap;
+  g->bk_send = send;
+  g->bk_recv = recv;
+  g->tot_send = tot_send;
+  g->tot_recv = tot_recv;
+  g->fill_params();
+  return CL_OK;
+}
+
+int cl_graph_part_dev_seal(cl_graph* g) {
+  G_DEV(g);
+  return g->k_err(cg_launch_part_dev_seal(g->P, g->stream));
+}
+
+int cl_graph_part_dev_pick(cl_graph* g) {
+  G_DEV(g);
+  if (g->time + 1 > kMaxGraphTime) return gerr(CL_E_LIMIT, "simulated time would exceed %lld ticks", (long long)kMaxGraphTime);
+  ++g->time;
+  return g->k_err(cg_launch_part_dev_pick(g->P, (int32_t)g->time, g->stream));
+}
+
+int cl_graph_part_dev_receive(cl_graph* g) {
+  G_DEV(g);
+  return g->k_err(cg_launch_part_dev_receive(g->P, (int32_t)g->time, g->stream));
+}
+
+int cl_graph_part_dev_tally(cl_graph* g, int32_t step) {
+  G_DEV(g);
+  return g->k_err(cg_launch_part_dev_tally(g->P, step, g->stream));
+}
+
+int cl_graph_part_dev_bases(cl_graph* g) {
+  G_DEV(g);
+  return g->k_err(cg_launch_part_dev_bases(g->P, g->stream));
+}
+
+int cl_graph_part_dev_push(cl_graph* g, int32_t step) {
+  G_DEV(g);
+  return g->k_err(cg_launch_part_dev_push(g->P, (int32_t)g->time, step, g->stream));
 }
 
 }  // extern "C"

@@ -136,6 +136,14 @@ __device__ inline bool traffic_send(const GParams& p, int64_t step, int32_t v, i
   return true;
 }
 
+// Append one row to the outgoing exchange bucket of rank q (partitioned mode, device
+// exchange).  The capacity is the topology's exact bound; a row past it freezes the run.
+__device__ inline void bucket_row(const GParams& p, int32_t q, int4 row) {
+  const uint32_t slot = atomicAdd(&p.bk_cnt[q], 1u);
+  if (slot < (uint32_t)p.bk_cap) p.bk_send[(size_t)q * (p.bk_cap + 1) + 1 + slot] = row;
+  else set_status(p.sc, kGStatusXchgOverflow);
+}
+
 // NotifyCompletedSnapshot (sim.go:126-131) for every lane with `done` (node v complete
 // in snapshot sid).  Two-level count, so no word sees more than a few hundred atomics: a
 // node completes its group of kGThreads node ranks, the group that fills completes one
@@ -385,7 +393,8 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
       const int32_t v = rte.x, k = rte.y;
       ++c[(pay & kGMarker) ? 2 : 1];
       if (v < p.part_lo || v >= p.part_hi) {  // partitioned: the receiver's device applies it
-        p.outbox[atomicAdd(&p.out_n[0], 1u)] = PDel{s, v, k, pay};
+        if (p.bk_send) bucket_row(p, v / p.bk_span, make_int4(s, v, k, (int)pay));
+        else p.outbox[atomicAdd(&p.out_n[0], 1u)] = PDel{s, v, k, pay};
         break;
       }
       ChIn* ci = &p.chin[k];
@@ -475,6 +484,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
       const int32_t od = p.out_off[v + 1] - p.out_off[v];
       if (!p.part) s_trig[s0 - bk * kGThreads] = od;
       else if (s0 >= p.part_lo && s0 < p.part_hi) p.trigv[s0] = od;  // (one delivery per sender and tick)
+      else if (p.bk_send) bucket_row(p, s0 / p.bk_span, make_int4(s0, od, 0, 0));
       else p.reports[atomicAdd(&p.out_n[2], 1u)] = make_int2(s0, od);
       if (p.trace)  // SendToNeighbors' SentMsgRecords (node.go:100)
         for (int32_t j = p.out_off[v]; j < p.out_off[v + 1]; ++j)
@@ -964,10 +974,7 @@ __global__ void __launch_bounds__(kGThreads) k_sg_apply(GParams p, int32_t time,
 // Deliveries by other devices' senders to owned receivers: k_pick's receiver half
 // (HandleToken node.go:174-185 on the token count and channel cursor; markers keyed and
 // staged for k_marker<true>).  Every channel carries at most one delivery per tick.
-__global__ void __launch_bounds__(kGThreads) k_part_apply(GParams p, int32_t t, const PDel* in, int32_t n_in) {
-  const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
-  if (i >= n_in || p.sc->status) return;
-  const PDel d = in[i];
+__device__ inline void apply_delivery(const GParams& p, int32_t t, const PDel d) {
   ChIn* ci = &p.chin[d.k];
   ci->tick = (uint32_t)t;
   ci->pay = d.pay;
@@ -984,6 +991,105 @@ __global__ void __launch_bounds__(kGThreads) k_part_apply(GParams p, int32_t t, 
     }
     ci->tokcnt = tc + 1;
   }
+}
+
+__global__ void __launch_bounds__(kGThreads) k_part_apply(GParams p, int32_t t, const PDel* in, int32_t n_in) {
+  const int32_t i = blockIdx.x * kGThreads + threadIdx.x;
+  if (i >= n_in || p.sc->status) return;
+  apply_delivery(p, t, in[i]);
+}
+
+// ---- device exchange (cl_graph_part_dev_*): fixed-capacity buckets, no host round trip ----
+// Row r of received bucket q (rows past the bucket's header count do not exist).
+__device__ inline bool bucket_in(const GParams& p, int64_t i, int32_t* q, int32_t* r, int4* row) {
+  if (i >= (int64_t)p.bk_world * p.bk_cap) return false;
+  *q = (int32_t)(i / p.bk_cap);
+  *r = (int32_t)(i % p.bk_cap);
+  const int4* b = p.bk_recv + (size_t)*q * (p.bk_cap + 1);
+  if (*r >= b[0].x) return false;
+  *row = b[1 + *r];
+  return true;
+}
+
+// Seal the outgoing buckets: header row = rows appended (counters reset for the next step).
+__global__ void k_bk_seal(GParams p) {
+  for (int32_t q = threadIdx.x; q < p.bk_world; q += blockDim.x) {
+    const uint32_t c = p.bk_cnt[q];
+    p.bk_send[(size_t)q * (p.bk_cap + 1)] = make_int4((int)min(c, (uint32_t)p.bk_cap), 0, 0, 0);
+    p.bk_cnt[q] = 0;
+  }
+}
+
+// Deliveries other devices' senders addressed to owned receivers (k_part_apply's rows).
+__global__ void __launch_bounds__(kGThreads) k_bk_apply(GParams p, int32_t t) {
+  int32_t q, r;
+  int4 d;
+  if (p.sc->status || !bucket_in(p, blockIdx.x * (int64_t)kGThreads + threadIdx.x, &q, &r, &d)) return;
+  apply_delivery(p, t, PDel{d.x, d.y, d.z, (uint32_t)d.w});
+}
+
+// Reports (s0, outdeg) about owned senders whose markers created snapshots on other devices.
+__global__ void __launch_bounds__(kGThreads) k_bk_trig(GParams p) {
+  int32_t q, r;
+  int4 d;
+  if (bucket_in(p, blockIdx.x * (int64_t)kGThreads + threadIdx.x, &q, &r, &d)) p.trigv[d.x] = d.y;
+}
+
+// This rank's tick totals for the all-gather (k_scan wrote them; a frozen run's are stale,
+// its status stops every rank).
+__global__ void k_bk_totals(GParams p) {
+  p.tot_send[0] = (long long)p.sc->tot_trig;
+  p.tot_send[1] = (long long)p.sc->tot_send;
+  p.tot_send[2] = p.sc->status;
+  p.tot_send[3] = 0;
+}
+
+// Global draw bases from every rank's totals (k_part_bases with the sums taken on the
+// device); a rank that froze stops every rank at the same step with its status.
+__global__ void k_bk_bases(GParams p) {
+  long long tb = 0, ta = 0, sb = 0, sa = 0, st = 0;
+  for (int32_t r = 0; r < p.bk_world; ++r) {
+    const long long* x = p.tot_recv + 4 * r;
+    ta += x[0];
+    sa += x[1];
+    if (r < p.bk_rank) {
+      tb += x[0];
+      sb += x[1];
+    }
+    st = max(st, x[2]);
+  }
+  if (st) {
+    if (!p.sc->status) p.sc->status = (int32_t)st;
+    return;
+  }
+  const unsigned long long d = p.sc->draw;
+  p.sc->base_trig = d + (unsigned long long)tb;
+  p.sc->base_send = d + (unsigned long long)(ta + sb);
+  p.sc->draw = d + (unsigned long long)(ta + sa);
+}
+
+// Replies: the first draw of each reported broadcast, back into the reporting rank's bucket
+// in report order.  Thread r = 0 of every bucket writes its header.
+__global__ void __launch_bounds__(kGThreads) k_bk_draws(GParams p) {
+  const int64_t i = blockIdx.x * (int64_t)kGThreads + threadIdx.x;
+  if (i >= (int64_t)p.bk_world * p.bk_cap) return;
+  const int32_t q = (int32_t)(i / p.bk_cap), r = (int32_t)(i % p.bk_cap);
+  const int4* b = p.bk_recv + (size_t)q * (p.bk_cap + 1);
+  const int32_t n = b[0].x;
+  int4* o = p.bk_send + (size_t)q * (p.bk_cap + 1);
+  if (r == 0) o[0] = make_int4(n, 0, 0, 0);
+  if (r >= n) return;
+  const int32_t s0 = b[1 + r].x;
+  const unsigned long long d = broadcast_draw(p, s0);
+  o[1 + r] = make_int4(s0, (int)(uint32_t)d, (int)(uint32_t)(d >> 32), 0);
+}
+
+// The replies to this rank's reports: first draws of broadcasts on remote senders' markers.
+__global__ void __launch_bounds__(kGThreads) k_bk_rdraw(GParams p) {
+  int32_t q, r;
+  int4 d;
+  if (bucket_in(p, blockIdx.x * (int64_t)kGThreads + threadIdx.x, &q, &r, &d))
+    p.rdraw[d.x] = (unsigned long long)(uint32_t)d.y | ((unsigned long long)(uint32_t)d.z << 32);
 }
 
 // Reports of broadcasts that other devices' receivers created on owned senders' markers.
@@ -1244,6 +1350,58 @@ int cg_launch_part_bases(const GParams& p, int64_t trig_before, int64_t trig_all
 int cg_launch_part_push(const GParams& p, int32_t t, int32_t step, const long long* replies, int32_t n, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n > 0) hipLaunchKernelGGL(k_part_rdraw, dim3((n + kGThreads - 1) / kGThreads), dim3(kGThreads), 0, s, p, replies, n);
+  launch_push(p, t, step, s);
+  return hipGetLastError();
+}
+
+// ---- device exchange steps (the collectives run between them on the same stream) ----
+static unsigned bk_grid(const GParams& p) {
+  const int64_t m = (int64_t)p.bk_world * p.bk_cap;
+  return (unsigned)((m + kGThreads - 1) / kGThreads);
+}
+
+int cg_launch_part_dev_seal(const GParams& p, void* stream) {
+  hipLaunchKernelGGL(k_bk_seal, dim3(1), dim3(64), 0, (hipStream_t)stream, p);
+  return hipGetLastError();
+}
+
+int cg_launch_part_dev_pick(const GParams& p, int32_t t, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if ((e = hipMemsetAsync(p.out_n, 0, 4 * sizeof(uint32_t), s))) return e;
+  if (p.blk_hi > p.blk_lo) launch_pick(p, dim3(p.blk_hi - p.blk_lo), t, s);
+  return cg_launch_part_dev_seal(p, stream);
+}
+
+int cg_launch_part_dev_receive(const GParams& p, int32_t t, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned g = bk_grid(p);
+  hipLaunchKernelGGL(k_bk_apply, dim3(g), dim3(kGThreads), 0, s, p, t);
+  if (p.blk_hi > p.blk_lo)
+    hipLaunchKernelGGL(k_marker<false>, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, t);
+  hipLaunchKernelGGL(k_marker<true>, dim3(g), dim3(kGThreads), 0, s, p, t);  // (blocks past out_n[1] return)
+  return cg_launch_part_dev_seal(p, stream);
+}
+
+int cg_launch_part_dev_tally(const GParams& p, int32_t step, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_bk_trig, dim3(bk_grid(p)), dim3(kGThreads), 0, s, p);
+  if (p.blk_hi > p.blk_lo) hipLaunchKernelGGL(k_tally, dim3(p.blk_hi - p.blk_lo), dim3(kGThreads), 0, s, p, step);
+  launch_scan(p, 0, 0, 0, s);
+  hipLaunchKernelGGL(k_bk_totals, dim3(1), dim3(1), 0, s, p);
+  return hipGetLastError();
+}
+
+int cg_launch_part_dev_bases(const GParams& p, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_bk_bases, dim3(1), dim3(1), 0, s, p);
+  hipLaunchKernelGGL(k_bk_draws, dim3(bk_grid(p)), dim3(kGThreads), 0, s, p);
+  return hipGetLastError();
+}
+
+int cg_launch_part_dev_push(const GParams& p, int32_t t, int32_t step, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_bk_rdraw, dim3(bk_grid(p)), dim3(kGThreads), 0, s, p);
   launch_push(p, t, step, s);
   return hipGetLastError();
 }

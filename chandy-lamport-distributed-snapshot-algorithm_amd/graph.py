@@ -81,6 +81,14 @@ def glib():
             "cl_graph_part_bases": [vp, vp, vp, i64, vp],
             "cl_graph_part_push": [vp, i32, vp, i64],
             "cl_graph_part_freeze": [vp, i32],
+            "cl_graph_part_dev_bind": [vp, i32, i32, i32, i64, vp, vp, vp, vp],
+            "cl_graph_part_dev_seal": [vp],
+            "cl_graph_part_dev_pick": [vp],
+            "cl_graph_part_dev_receive": [vp],
+            "cl_graph_part_dev_tally": [vp, i32],
+            "cl_graph_part_dev_bases": [vp],
+            "cl_graph_part_dev_push": [vp, i32],
+            "cl_graph_set_stream": [vp, vp],
         }
         for name, args in sig.items():
             f = getattr(L, name)
@@ -103,6 +111,7 @@ class GraphSim:
         h = C.c_void_p()
         _check(self._L.cl_graph_create(C.byref(h)))
         self._h = h
+        self.device = device
         _check(self._L.cl_graph_set_device(self._h, device))
         _check(self._L.cl_graph_set_limits(self._h, fifo_slots, max_snapshots, max_drain_ticks))
         self._ids = None
@@ -356,10 +365,13 @@ class PartitionedGraphSim:
     steps restate the tick of sim.go:71-95 across ranks (tests/partition_model.py is the
     same protocol on the CPU)."""
 
-    def __init__(self, sim, rank, world, exchange_device="cpu"):
+    def __init__(self, sim, rank, world, exchange_device="cpu", transport="host"):
         from . import dist as D
+        if transport not in ("host", "device"):
+            raise ValueError(f"transport {transport!r}: 'host' or 'device'")
         self.D, self.g, self.rank, self.world = D, sim, rank, world
         self.dev = exchange_device
+        self.transport = transport
         n = sim.num_nodes
         blocks = -(-n // 256)
         per = -(-blocks // world)
@@ -372,7 +384,80 @@ class PartitionedGraphSim:
         _check(self._L.cl_graph_part_begin(sim._h, self.lo, self.hi))
         self.time = 0
         self.n_sids = 0
-        self.frozen = 0
+        self._frozen = 0
+        if transport == "device":
+            self._dev_setup()
+
+    @property
+    def frozen(self):
+        """Nonzero once the run stopped (every rank stops at the same step).  The device
+        transport decides it on the device (cl_graph_part_dev_bases): read back here."""
+        return self.g.status() if self.transport == "device" else self._frozen
+
+    # ---- device-resident exchange (clgraph.h cl_graph_part_dev_*) ----------------------
+    def bucket_capacity(self):
+        """Rows per exchange bucket: the most nodes of one rank with a channel into another
+        rank's nodes -- each sender delivers at most one packet per tick, so this bounds the
+        deliveries, the broadcast reports and the replies between any two ranks."""
+        src, dst = self.g.channels()
+        w = self.world
+        key = np.unique(src.astype(np.int64) * w + dst.astype(np.int64) // self.span)
+        pair = (key // w) // self.span * w + key % w
+        cnt = np.bincount(pair, minlength=w * w).reshape(w, w)
+        np.fill_diagonal(cnt, 0)
+        return max(int(cnt.max()), 1)
+
+    def _dev_setup(self):
+        import torch
+        dev = torch.device("cuda", self.g.device)
+        self.cap = self.bucket_capacity()
+        rows = self.world * (self.cap + 1)
+        self._send = torch.zeros(2 * rows, dtype=torch.int64, device=dev)    # 16-B rows
+        self._recv = torch.zeros_like(self._send)
+        self._tsend = torch.zeros(4, dtype=torch.int64, device=dev)
+        self._trecv = torch.zeros(4 * self.world, dtype=torch.int64, device=dev)
+        self._stream = torch.cuda.Stream(device=dev)
+        self.g._stream_ref = self._stream          # (outlives the engine's use of it)
+        _check(self._L.cl_graph_set_stream(self.g._h, C.c_void_p(self._stream.cuda_stream)))
+        _check(self._L.cl_graph_part_dev_bind(self.g._h, self.world, self.rank, self.span, self.cap,
+                                              C.c_void_p(self._send.data_ptr()), C.c_void_p(self._recv.data_ptr()),
+                                              C.c_void_p(self._tsend.data_ptr()), C.c_void_p(self._trecv.data_ptr())))
+
+    def _a2a(self):
+        """Bucket q of send to rank q, rank q's bucket for this rank into recv bucket q (RCCL
+        on the device buffers; gloo rehearsals stage them through host memory)."""
+        import torch
+        import torch.distributed as dist
+        with torch.cuda.stream(self._stream):
+            if self.dev == "cuda":
+                dist.all_to_all_single(self._recv, self._send)
+            else:
+                h = self._send.cpu()                # (after the engine's launches on this stream)
+                r = torch.empty_like(h)
+                dist.all_to_all_single(r, h)
+                self._recv.copy_(r)
+
+    def _gather(self):
+        import torch
+        import torch.distributed as dist
+        with torch.cuda.stream(self._stream):
+            if self.dev == "cuda":
+                dist.all_gather_into_tensor(self._trecv, self._tsend)
+            else:
+                h = self._tsend.cpu()
+                out = [torch.empty_like(h) for _ in range(self.world)]
+                dist.all_gather(out, h)
+                self._trecv.copy_(torch.cat(out))
+
+    def _dev_finish(self, step):
+        """reports -> tally -> totals -> bases + replies -> push, all on the device."""
+        L, h = self._L, self.g._h
+        self._a2a()
+        _check(L.cl_graph_part_dev_tally(h, step))
+        self._gather()
+        _check(L.cl_graph_part_dev_bases(h))
+        self._a2a()
+        _check(L.cl_graph_part_dev_push(h, step))
 
     def owner(self, v):
         return np.asarray(v) // self.span
@@ -395,7 +480,7 @@ class PartitionedGraphSim:
         if frozen:                  # a device froze (its totals are stale): every device stops here
             if not tot[2]:
                 _check(self._L.cl_graph_part_freeze(self.g._h, frozen))
-            self.frozen = frozen
+            self._frozen = frozen
             return
         r = self.rank
         bases = np.array([allt[:r, 0].sum(), allt[:, 0].sum(), allt[:r, 1].sum(), allt[:, 1].sum()], dtype=np.int64)
@@ -415,6 +500,10 @@ class PartitionedGraphSim:
 
     def start(self):
         """The step-0 traffic (the whole-graph engine runs it at reset)."""
+        if self.transport == "device":
+            _check(self._L.cl_graph_part_dev_seal(self.g._h))      # no reports
+            self._dev_finish(0)
+            return
         self._finish_step(0, [np.zeros((0, 2), dtype=np.int64)] * self.world)
 
     def start_snapshot_rank(self, node):            # sim.go:105 (called on every rank)
@@ -424,9 +513,16 @@ class PartitionedGraphSim:
         return sid.value
 
     def tick(self):                                 # sim.go:71-95 across the ranks
-        if self.frozen:                             # (the run stopped on every rank)
-            return
         h = self.g._h
+        if self.transport == "device":              # no host round trip (a frozen run's kernels return)
+            _check(self._L.cl_graph_part_dev_pick(h))
+            self.time += 1
+            self._a2a()
+            _check(self._L.cl_graph_part_dev_receive(h))
+            self._dev_finish(self.time)
+            return
+        if self._frozen:                            # (the run stopped on every rank)
+            return
         out = np.zeros((max(self.hi - self.lo, 1), 4), dtype=np.int32)
         m = C.c_int64(0)
         _check(self._L.cl_graph_part_pick(h, _p(out), out.shape[0], C.byref(m)))

@@ -202,6 +202,41 @@ int cl_graph_part_push(cl_graph* g, int32_t step, const int64_t* replies, int64_
  * another device froze, and the partitioned run stops everywhere at the same step. */
 int cl_graph_part_freeze(cl_graph* g, int32_t status);
 
+/* ---- partitioned mode, device-resident exchange ---------------------------------------
+ * The same tick with every exchanged row kept in device memory: the caller binds four
+ * device buffers it owns (torch tensors) and runs the collectives between the steps on
+ * the engine's stream (cl_graph_set_stream: torch's current stream), so a tick needs no
+ * host round trip (RCCL all-to-all / all-gather over xGMI with one process per GPU).
+ *   send, recv  world * (cap + 1) rows of 16 B each: bucket q = a header row {rows, 0, 0, 0},
+ *               then up to `cap` rows; send bucket q goes to rank q and recv bucket q came
+ *               from rank q (all_to_all_single with equal splits);
+ *   tot_send    4 int64 (this rank's trigger draws, send draws, status, 0);
+ *   tot_recv    world * 4 int64 (all_gather of tot_send).
+ * `cap` must bound every bucket: for ranks r != q, the number of r's nodes with a channel
+ * into q's nodes (graph.py computes it from the topology); `span` = nodes per rank
+ * (owner(v) = v / span, the block-aligned ranges of part_begin).  One tick:
+ *   dev_pick      time++, pops; deliveries to other ranks' receivers -> send       [all-to-all]
+ *   dev_receive   recv deliveries + own markers; broadcast reports (s0, outdeg) -> send
+ *                                                                                  [all-to-all]
+ *   dev_tally     recv reports, tally of triggers and next-step sends -> tot_send  [all-gather]
+ *   dev_bases     draw bases from tot_recv (a frozen rank freezes every rank); replies
+ *                 (s0, first draw) to the reporters -> send                       [all-to-all]
+ *   dev_push      recv replies; pushes of broadcasts and the traffic of `step`.
+ * The step-0 traffic: dev_seal (empty reports) [all-to-all] dev_tally(0) [all-gather]
+ * dev_bases [all-to-all] dev_push(0).  The results are part_* queries as above. */
+int cl_graph_part_dev_bind(cl_graph* g, int32_t world, int32_t rank, int32_t span, int64_t cap, void* send,
+                           void* recv, void* tot_send, void* tot_recv);
+int cl_graph_part_dev_seal(cl_graph* g);
+int cl_graph_part_dev_pick(cl_graph* g);
+int cl_graph_part_dev_receive(cl_graph* g);
+int cl_graph_part_dev_tally(cl_graph* g, int32_t step);
+int cl_graph_part_dev_bases(cl_graph* g);
+int cl_graph_part_dev_push(cl_graph* g, int32_t step);
+/* Run every later launch and copy of this engine on `stream` (a hipStream_t of the engine's
+ * device, e.g. torch.cuda.current_stream().cuda_stream; NULL = the engine's own stream).
+ * The engine waits for its own stream first. */
+int cl_graph_set_stream(cl_graph* g, void* stream);
+
 /* ---- counter hash of the synthetic workloads ------------------------------------ */
 uint64_t cl_counter_hash(uint64_t seed, uint64_t a, uint64_t b);
 

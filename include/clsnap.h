@@ -62,6 +62,7 @@ extern "C" {
 #define CL_INST_HANG 4                      /* drain exceeded max ticks (test_common.go:124-132 loops forever) */
 #define CL_INST_DELAY_EXHAUSTED 5           /* replayed delay schedule too short */
 #define CL_INST_HIST_OVERFLOW 6             /* graph engine: token history slots exhausted */
+#define CL_INST_XCHG_OVERFLOW 7             /* partitioned graph run: a device exchange bucket overflowed */
 
 /* ---- counters (cl_get_counters), summed over instances ------------------ */
 #define CL_CNT_PUSH 0      /* Queue.Push (queue.go:18) == delay draws (sim.go:101) */

@@ -5,8 +5,12 @@ over gloo (graph.py PartitionedGraphSim -> cl_graph_part_*).  The gathered run m
 the oracle's unpartitioned run bit for bit: status, time, final tokens, completion ticks,
 snapshot token maps, per-channel recorded messages and the reference counters.
 
-The 8-GPU form (one rank per GPU, exchange over RCCL) is the same code with
-exchange_device="cuda"; it is not measured."""
+Both transports are covered: "host" stages every exchanged row through host arrays;
+"device" keeps them in device buffers (cl_graph_part_dev_*: fixed-capacity buckets, the
+collectives on the engine's stream, no host round trip per tick), here with gloo staging
+the buckets through host memory since the ranks share one GPU.  The 8-GPU form (one rank
+per GPU, RCCL on the device buffers) is the same code with exchange_device="cuda"; it is
+not measured."""
 import os
 import socket
 
@@ -43,14 +47,14 @@ def _worker(rank, world, port, case, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import graphcheck as GC
-        kind, n, steps, seed, _, lanes, drain = case
+        kind, n, steps, seed, _, lanes, drain, transport = case
         p = _program(kind, n, steps, seed)
         g = GC.clg.GraphSim(device=0, fifo_slots=p.fifo_slots, max_snapshots=len(p.snap_step))
         g.set_push_lanes(lanes)
         g.set_topology(p.tokens, p.src, p.dst, id_width=p.width())
         g.set_delay_hash(p.delay_seed)
         g.set_traffic(p.traffic_seed, p.thresh, p.traffic_steps)
-        ps = GC.clg.PartitionedGraphSim(g, rank, world)
+        ps = GC.clg.PartitionedGraphSim(g, rank, world, transport=transport)
         ps.run_program(p.steps, p.snap_step, p.snap_rank)
         if drain:
             assert ps.drain()
@@ -64,14 +68,17 @@ def _worker(rank, world, port, case, out):
         dist.destroy_process_group()
 
 
-CASES = [("regular", 4096, 90, 3, 2, 0, False), ("regular", 4096, 100, 5, 3, 1, False),
-         ("powerlaw", 2000, 300, 7, 2, 0, False), ("powerlaw", 2000, 70, 9, 2, 4, True)]
+CASES = [("regular", 4096, 90, 3, 2, 0, False, "host"), ("regular", 4096, 100, 5, 3, 1, False, "host"),
+         ("powerlaw", 2000, 300, 7, 2, 0, False, "host"), ("powerlaw", 2000, 70, 9, 2, 4, True, "host"),
+         ("regular", 4096, 90, 3, 2, 0, False, "device"), ("regular", 4096, 100, 5, 3, 1, False, "device"),
+         ("powerlaw", 2000, 300, 7, 2, 0, False, "device"), ("powerlaw", 2000, 70, 9, 3, 4, True, "device")]
 
 
-@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}{c[1]}_w{c[4]}_l{c[5]}{'_drain' if c[6] else ''}")
+@pytest.mark.parametrize("case", CASES,
+                         ids=lambda c: f"{c[0]}{c[1]}_w{c[4]}_l{c[5]}{'_drain' if c[6] else ''}_{c[7]}")
 def test_partitioned_device_run_vs_oracle(case):
     import graphcheck as GC
-    kind, n, steps, seed, world, _, drain = case
+    kind, n, steps, seed, world, _, drain, _ = case
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), case, out), nprocs=world, join=True)
@@ -98,7 +105,7 @@ def test_partitioned_device_run_vs_oracle(case):
         np.testing.assert_array_equal(vals, ovals)
 
 
-def _freeze_worker(rank, world, port, out):
+def _freeze_worker(rank, world, port, transport, out):
     import sys
     for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
@@ -112,7 +119,7 @@ def _freeze_worker(rank, world, port, out):
         g.set_topology(p.tokens, p.src, p.dst, id_width=p.width())
         g.set_delay_hash(p.delay_seed)
         g.set_traffic(p.traffic_seed, p.thresh, p.traffic_steps)
-        ps = GC.clg.PartitionedGraphSim(g, rank, world)
+        ps = GC.clg.PartitionedGraphSim(g, rank, world, transport=transport)
         ps.run_program(p.steps, p.snap_step, p.snap_rank)
         out[rank] = (g.status(), ps.frozen, ps.time)
     except Exception as e:  # surfaced in the parent
@@ -122,7 +129,8 @@ def _freeze_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_partitioned_freeze_stops_every_rank():
+@pytest.mark.parametrize("transport", ["host", "device"])
+def test_partitioned_freeze_stops_every_rank(transport):
     """Four FIFO slots per channel overflow at the power-law hubs on one rank (an engine
     limit, CL_INST_FIFO_OVERFLOW): the status is allgathered with the tick totals, so every
     rank stops at the same step with the same status instead of drawing from the frozen
@@ -130,7 +138,7 @@ def test_partitioned_freeze_stops_every_rank():
     import graphcheck as GC
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_freeze_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_freeze_worker, args=(2, _free_port(), transport, out), nprocs=2, join=True)
     (s0, f0, t0), (s1, f1, t1) = out[0], out[1]
     assert f0 == f1 != 0 and s0 == s1 == f0 and t0 == t1
     p = _program("powerlaw", 2000, 120, 9)
