@@ -69,14 +69,11 @@ struct PDel {
   uint32_t pay;
 };
 
-// Per in-channel record, by in-CSR position (16 B, one access per delivery / per
-// expanded in-link).
-struct ChIn {
-  uint32_t tokcnt;  // tokens delivered on the channel so far (the recording cursor)
-  uint32_t tick;    // tick of the latest delivery on the channel
-  uint32_t pay;     // payload word of that delivery (kGMarker | sid, or token count)
-  int32_t src;      // sender rank (topology)
-};
+// Receiver-side channel state is one word per in-channel, tokcnt[k]: the tokens delivered on
+// it so far (the recording cursor).  A local snapshot created this tick learns whether its
+// in-channel k also delivered this tick, and what, from the SENDER's delivery word: sender
+// s = in_src[k] popped on out-link in_oj[k] this tick iff pick[s] == (t << 6) | in_oj[k],
+// with payload ppay[s] (each sender delivers at most once per tick, sim.go:90).
 
 constexpr uint32_t kEmpty = 0xffffffffu;  // head receiveTime word of an empty channel
 
@@ -151,10 +148,12 @@ struct GParams {
   const int32_t* out_off;   // [n+1]
   const int2* route;        // [e] channel c: (dest rank, in-CSR position)
   const int32_t* in_off;    // [n+1]
-  const int32_t* in_src;    // [e] src rank at in-position k (reset source for chin[].src)
+  const int32_t* in_src;    // [e] src rank at in-position k
+  const uint8_t* in_oj;     // [e] out-link index at the sender of in-position k
   // node state
   int32_t* tokens;     // [n]
   int32_t* pick;       // [n] (tick << 6) | out-index popped in that tick
+  uint32_t* ppay;      // [n] payload word of that pop (kGMarker | sid, or token count)
   int32_t* ltrig;      // [n] block-local exclusive prefix of triggered broadcasts (draws)
   int32_t* lsend;      // [n] block-local exclusive prefix of traffic sends
   long long* bsum;     // [2 * n_pblocks] block sums (trig, send) -> exclusive block offsets
@@ -169,7 +168,7 @@ struct GParams {
   //     hi32: ring head (lo16) | packets queued (hi16)
   uint64_t* hq;
   uint64_t* fifo;      // [e << cap_log2]
-  ChIn* chin;          // [e] by in-position
+  uint32_t* tokcnt;    // [e] by in-position: tokens delivered on the channel so far
   uint32_t* histv;     // [e * hist] by in-position
   // snapshot state
   uint64_t* W;         // [s_cap * n] creation key: (tick << 32) | creating sender (initiator: | 0xffffffff)

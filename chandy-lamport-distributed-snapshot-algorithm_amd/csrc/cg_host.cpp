@@ -165,7 +165,8 @@ struct cl_graph {
   GBuf<int2> d_route;
   GBuf<int32_t> d_tokens, d_pick, d_ltrig, d_lsend, d_crn, d_mcnt;
   GBuf<MDel> d_mlist;
-  GBuf<ChIn> d_chin;
+  GBuf<uint32_t> d_tokcnt, d_ppay;
+  GBuf<uint8_t> d_in_oj;
   GBuf<BigX> d_big;
   GBuf<unsigned long long> d_cpart;
   GBuf<uint64_t> d_cre;
@@ -208,7 +209,7 @@ struct cl_graph {
                              &d_done,    &d_ctick};
     for (auto* b : i32s) b->release();
     d_cre.release(); d_bsum.release(); d_hq.release(); d_histv.release(); d_mlist.release(); d_route.release();
-    d_chin.release(); d_fifo.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
+    d_tokcnt.release(); d_ppay.release(); d_in_oj.release(); d_fifo.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
     d_sched.release(); d_scratch.release(); d_big.release(); d_cpart.release();
     d_trace.release(); d_trace_cnt.release();
     d_outbox.release(); d_inbox.release(); d_out_n.release(); d_rmlist.release(); d_reports.release();
@@ -419,8 +420,12 @@ struct cl_graph {
     int rc;
     std::vector<int2> route((size_t)e);
     for (int64_t c = 0; c < e; ++c) route[c] = make_int2(ch_dst[c], ch_inpos[c]);
+    // out-link index at the sender of every in-channel (expansions match it against the
+    // sender's delivery word; out-degrees are below 256: kGMaxOutDegree)
+    std::vector<uint8_t> in_oj((size_t)e);
+    for (int64_t c = 0; c < e; ++c) in_oj[(size_t)ch_inpos[c]] = (uint8_t)(c - out_off[ch_src[c]]);
     if ((rc = d_out_off.upload(out_off)) || (rc = d_route.upload(route)) || (rc = d_in_off.upload(in_off)) ||
-        (rc = d_in_src.upload(in_src)) || (rc = d_init_tok.upload(init_tok)))
+        (rc = d_in_src.upload(in_src)) || (rc = d_in_oj.upload(in_oj)) || (rc = d_init_tok.upload(init_tok)))
       return rc;
     return CL_OK;
   }
@@ -459,7 +464,7 @@ struct cl_graph {
         (rc = d_lsend.ensure(N)) || (rc = d_crn.ensure(N)) || (rc = d_mlist.ensure(NP * kGThreads)) ||
         (rc = d_mcnt.ensure(NP)) || (rc = d_big.ensure(N)) || (rc = d_cpart.ensure((size_t)kParts * kNumCnt)) ||
         (rc = d_cre.ensure(E)) || (rc = d_bsum.ensure(2 * NP)) || (rc = d_hq.ensure(E)) ||
-        (rc = d_chin.ensure(E)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
+        (rc = d_tokcnt.ensure(E)) || (rc = d_ppay.ensure(N)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
         (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_W.ensure(s_cap * N)) ||
         (rc = d_rec.ensure(s_cap * E)) || (rc = d_cnt.ensure(s_cap * N)) || (rc = d_stok.ensure(s_cap * N)) ||
         (rc = d_done.ensure((size_t)s_cap * (1 + NP))) || (rc = d_ctick.ensure(s_cap)) || (rc = d_sc.ensure(1)) ||
@@ -524,7 +529,9 @@ struct cl_graph {
     p.cpart = d_cpart.p;
     p.hq = d_hq.p;
     p.fifo = d_fifo.p;
-    p.chin = d_chin.p;
+    p.tokcnt = d_tokcnt.p;
+    p.ppay = d_ppay.p;
+    p.in_oj = d_in_oj.p;
     p.histv = d_histv.p;
     p.W = d_W.p;
     p.cnt = d_cnt.p;
@@ -1262,7 +1269,7 @@ int cl_graph_device_bytes(cl_graph* g, int64_t* bytes) {
   if (!bytes) return gerr(CL_E_INVALID, "null output");
   size_t b = 0;
   b += g->d_out_off.bytes() + g->d_route.bytes() + g->d_in_off.bytes() +
-       g->d_in_src.bytes() + g->d_init_tok.bytes() + g->d_tokens.bytes() + g->d_pick.bytes() + g->d_chin.bytes() +
+       g->d_in_src.bytes() + g->d_init_tok.bytes() + g->d_tokens.bytes() + g->d_pick.bytes() + g->d_tokcnt.bytes() + g->d_ppay.bytes() + g->d_in_oj.bytes() +
        g->d_ltrig.bytes() + g->d_lsend.bytes() + g->d_crn.bytes() + g->d_mlist.bytes() + g->d_mcnt.bytes() +
        g->d_big.bytes() + g->d_cpart.bytes() +
        g->d_cre.bytes() + g->d_bsum.bytes() + g->d_hq.bytes() +

@@ -229,14 +229,15 @@ __device__ inline int expand_range(const GParams& p, int32_t t, int32_t s0, int3
   int tsum = 0;
   uint64_t* rec = p.rec + (size_t)sid * p.e;
   for (int32_t k = lo; k < hi; k += step) {
-    const ChIn ci = p.chin[k];
-    uint32_t b = ci.tokcnt;
+    uint32_t b = p.tokcnt[k];
     bool closed = k == karr;  // the arriving channel does not record (node.go:66-69)
-    if (ci.tick == (uint32_t)t && ci.src > s0) {
-      if (!(ci.pay & kGMarker)) {
+    const int32_t src = p.in_src[k];
+    if (src > s0 && p.pick[src] == ((t << 6) | (int32_t)p.in_oj[k])) {  // a later delivery this tick
+      const uint32_t pay = p.ppay[src];
+      if (!(pay & kGMarker)) {
         b -= 1;  // delivered after the creating marker: recorded
-        tsum += (int)ci.pay;
-      } else if ((int32_t)(ci.pay & kGPayload) == sid) {
+        tsum += (int)pay;
+      } else if ((int32_t)(pay & kGPayload) == sid) {
         closed = true;  // its own marker arrives later in the same tick
       }
     }
@@ -316,7 +317,7 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
     p.crn[i] = 0;
   }
   if (i < (size_t)p.e) {
-    p.chin[i] = ChIn{0u, 0u, 0u, p.in_src[i]};
+    p.tokcnt[i] = 0u;
     p.hq[i] = kEmpty;
   }
   if (i < (size_t)p.s_cap) p.ctick[i] = -1;
@@ -390,6 +391,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
       const uint32_t nrt = cnt ? (uint32_t)(p.fifo[ring + ((head + 1) & capm)] >> 32) : kEmpty;
       p.hq[ch] = ((uint64_t)(((head + 1) & capm) | (cnt << 16)) << 32) | nrt;
       p.pick[s] = (t << 6) | j;
+      p.ppay[s] = pay;
       const int32_t v = rte.x, k = rte.y;
       ++c[(pay & kGMarker) ? 2 : 1];
       if (v < p.part_lo || v >= p.part_hi) {  // partitioned: the receiver's device applies it
@@ -397,9 +399,6 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
         else p.outbox[atomicAdd(&p.out_n[0], 1u)] = PDel{s, v, k, pay};
         break;
       }
-      ChIn* ci = &p.chin[k];
-      ci->tick = (uint32_t)t;
-      ci->pay = pay;
       // ReceivedMsgRecord (sim.go:86)
       gtrace(p, t, kTrTick, (uint32_t)s, 0u, (pay & kGMarker) ? TK_RECV_MARKER : TK_RECV_TOKEN, v, s,
              (int32_t)(pay & kGPayload));
@@ -409,12 +408,12 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
         p.mlist[bk * kGThreads + atomicAdd(&s_m, 1)] = MDel{s, v, k, sid};
       } else {
         atomicAdd(&p.tokens[v], (int32_t)pay);  // HandleToken node.go:175
-        const uint32_t tc = ci->tokcnt;
+        const uint32_t tc = p.tokcnt[k];
         if (p.hist) {
           if (tc < (uint32_t)p.hist) p.histv[(size_t)k * p.hist + tc] = pay;
           else set_status(p.sc, kGStatusHistOverflow);
         }
-        ci->tokcnt = tc + 1;
+        p.tokcnt[k] = tc + 1;
       }
       break;
     }
@@ -503,7 +502,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
     } else {
       // later marker: stop recording the channel (node.go:158-160)
       if ((key >> 32) != (uint64_t)t) {  // created in an earlier tick: cursors exist
-        const uint32_t e = p.chin[k].tokcnt;
+        const uint32_t e = p.tokcnt[k];
         uint32_t* r = (uint32_t*)&p.rec[(size_t)sid * p.e + k];
         c[0] += e - r[0];
         r[1] = e;
@@ -887,7 +886,7 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
       const int32_t lo = p.in_off[v], hi = p.in_off[v + 1];
       uint64_t* rec = p.rec + (size_t)sid * p.e;
       for (int32_t k = lo + (int32_t)threadIdx.x; k < hi; k += blockDim.x)
-        rec[k] = (uint64_t)p.chin[k].tokcnt | ((uint64_t)kOpen << 32);
+        rec[k] = (uint64_t)p.tokcnt[k] | ((uint64_t)kOpen << 32);
       if (threadIdx.x == 0) {
         gtrace(p, time, kTrHost, (uint32_t)(ob + i), 0u, TK_START, v, -1, sid);  // sim.go:109
         for (int32_t j = 0; j < od && p.trace; ++j)  // SendToNeighbors (node.go:100)
@@ -975,21 +974,21 @@ __global__ void __launch_bounds__(kGThreads) k_sg_apply(GParams p, int32_t time,
 // (HandleToken node.go:174-185 on the token count and channel cursor; markers keyed and
 // staged for k_marker<true>).  Every channel carries at most one delivery per tick.
 __device__ inline void apply_delivery(const GParams& p, int32_t t, const PDel d) {
-  ChIn* ci = &p.chin[d.k];
-  ci->tick = (uint32_t)t;
-  ci->pay = d.pay;
+  // the remote sender's delivery word, on this device, for the expansions here
+  p.pick[d.s] = (t << 6) | (int32_t)p.in_oj[d.k];
+  p.ppay[d.s] = d.pay;
   if (d.pay & kGMarker) {
     const int32_t sid = (int32_t)(d.pay & kGPayload);
     atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + d.v], ((unsigned long long)t << 32) | (uint32_t)d.s);
     p.rmlist[atomicAdd(&p.out_n[1], 1u)] = MDel{d.s, d.v, d.k, sid};
   } else {
     atomicAdd(&p.tokens[d.v], (int32_t)d.pay);
-    const uint32_t tc = ci->tokcnt;
+    const uint32_t tc = p.tokcnt[d.k];
     if (p.hist) {
       if (tc < (uint32_t)p.hist) p.histv[(size_t)d.k * p.hist + tc] = d.pay;
       else set_status(p.sc, kGStatusHistOverflow);
     }
-    ci->tokcnt = tc + 1;
+    p.tokcnt[d.k] = tc + 1;
   }
 }
 
@@ -1135,7 +1134,7 @@ __global__ void k_finish(GParams p, int32_t n_sids, unsigned long long* out) {
     const uint64_t* r = p.rec + (size_t)sid * p.e;
     for (int32_t k = p.in_off[v]; k < p.in_off[v + 1]; ++k) {
       const uint64_t x = r[k];
-      if ((uint32_t)(x >> 32) == kOpen) rec += p.chin[k].tokcnt - (uint32_t)x;
+      if ((uint32_t)(x >> 32) == kOpen) rec += p.tokcnt[k] - (uint32_t)x;
     }
   }
   wave_count(out, rec);
