@@ -97,6 +97,8 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fresh", action="store_true", help="skip the fresh-seed first-launch measurement")
     ap.add_argument("--no-collect", action="store_true", help="skip the full-batch CollectSnapshot measurement")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="graph configs: skip the after-timing parity run (profiler passes that must see one program)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo for rehearsals")
     ap.add_argument("--shared-device", action="store_true",
                     help="every rank on cuda:0 (multi-rank rehearsal on a one-GPU box)")
@@ -420,7 +422,8 @@ def bench_graph(args, rank, world, local_rank):
     (pre_ms, pre_ticks), (drain_ms, drain_ticks) = g.phase_time()   # the last timed run
     sums = g.checksums()
     status = g.status()
-    parity, parity_ref = graph_parity(args.config, g, rank, n, steps, device)
+    parity, parity_ref = (None, "skipped (--no-parity)") if args.no_parity else \
+        graph_parity(args.config, g, rank, n, steps, device)
     vals = [sums[k] for k in clg.GSUM_NAMES]
     t_max, red = cldist.reduce_results(elapsed, vals, coll_dev)
     tot = dict(zip(clg.GSUM_NAMES, red))

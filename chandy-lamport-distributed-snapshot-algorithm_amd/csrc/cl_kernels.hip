@@ -566,6 +566,9 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
 #ifndef CLSNAP_SPLIT
 #define CLSNAP_SPLIT 1  // A/B knob: 0 replays a batch with spilling instances wholly on the spill-capable kernel
 #endif
+#ifndef CLSNAP_SPILL_FIRST
+#define CLSNAP_SPILL_FIRST 1  // split replays: dispatch the spill-capable (longest) instances first
+#endif
 #ifndef CLSNAP_W4NS
 #define CLSNAP_W4NS 6  // D = 3, 4 spill-free (the main pass of BASELINE config 3): 6 waves/SIMD
 #endif
@@ -1027,9 +1030,10 @@ __global__ __launch_bounds__(256) void cl_pack_fill(PackParams p) {
 
 }  // namespace
 
+// `stream`: launch there instead of L.stream, without the timing events unless `events`.
 template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true>
 int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L,
-                   void* stream = nullptr) {
+                   void* stream = nullptr, bool events = false) {
   const int32_t wpb = p.lay.wpb;
   const size_t lds = (size_t)p.lay.wave_words * wpb * sizeof(uint32_t);
   auto* k = cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>;
@@ -1040,8 +1044,9 @@ int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, con
   const int64_t waves = (p.n_inst - p.slot_base + p.lay.ipw - 1) / p.lay.ipw;
   const unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
   if (blocks == 0) return 0;
+  const bool ev = !stream || events;
   hipExtLaunchKernelGGL(k, dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)(stream ? stream : L.stream),
-                        (hipEvent_t)(stream ? nullptr : L.ev_start), (hipEvent_t)(stream ? nullptr : L.ev_stop), 0u, p,
+                        (hipEvent_t)(ev ? L.ev_start : nullptr), (hipEvent_t)(ev ? L.ev_stop : nullptr), 0u, p,
                         topo, ops, sched);
   return (int)hipGetLastError();
 }
@@ -1063,9 +1068,20 @@ int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, 
   b.slot_base = (uint32_t)p.split_slot;
   ExecLaunch la = L;
   la.ev_stop = nullptr;
-  int e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la);
-  if (e) return e;
-  if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, L, s2))) return e;
+  int e;
+  if (CLSNAP_SPILL_FIRST) {
+    // the spilling instances are the longest: their kernel is dispatched first so its
+    // workgroups are resident from the start instead of queueing behind the main grid (the
+    // tail of a small per-GPU batch); it records the start event
+    ExecLaunch lb = L;
+    lb.ev_stop = nullptr;
+    if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
+    la.ev_start = nullptr;
+    if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
+  } else {
+    if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
+    if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, L, s2))) return e;
+  }
   if ((he = hipEventRecord((hipEvent_t)L.ev_join, s2)) || (he = hipStreamWaitEvent(s, (hipEvent_t)L.ev_join, 0)))
     return (int)he;
   if (L.ev_stop && (he = hipEventRecord((hipEvent_t)L.ev_stop, s))) return (int)he;

@@ -1,8 +1,8 @@
 # PMC passes over a short bench run (each pass in its own rocprofv3 run; see MI355X_MICROARCH.md)
-# usage: CFG=c2|c3 bash tools/gpu_pmc.sh   -> gpurun_out/pmc_<cfg>/pass*/
+# usage: CFG=c2|c3 [SUFFIX=_x EXTRA="--instances N"] bash tools/gpu_pmc.sh   -> gpurun_out/pmc_<cfg><suffix>/pass*/
 set -e
 CFG=${CFG:-c2}
-OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_$CFG
+OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_$CFG${SUFFIX}
 rm -rf $OUT; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 ARGS="--config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-fresh ${EXTRA}"

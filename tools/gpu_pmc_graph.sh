@@ -7,6 +7,6 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/pmcg_$CFG
 rm -rf $OUT; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 P=$GRAFT_REPO_ROOT/bench.py
-ARGS="--config $CFG --steps 1 --warmup 0 --no-cpu-baseline"
+ARGS="--config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-parity"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pass3 -o p -- python3 $P $ARGS > $OUT/pass3.log 2>&1
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pass4 -o p -- python3 $P $ARGS > $OUT/pass4.log 2>&1

@@ -1,6 +1,7 @@
 """Turn a gpurun_out/pmc_<cfg> directory into committed profile summaries.
 
-usage: python tools/make_profiles.py <round> <cfg> [instances] [timed steps] [dispatches per step]
+usage: python tools/make_profiles.py <round> <cfg> [instances] [timed steps] [dispatches per step] [dir suffix]
+(reads gpurun_out/pmc_<cfg><dir suffix>, the directory tools/gpu_pmc.sh wrote with SUFFIX=...)
 writes profiles/<round>_<cfg>_kernel_stats.csv  (rocprofv3 --kernel-trace --stats)
        profiles/<round>_<cfg>_pmc.json          (per-dispatch PMC means, timed dispatches)
        profiles/traffic_<cfg>.json              (HBM bytes per launch for bench.py)
@@ -33,7 +34,7 @@ def per_dispatch(paths):
 def main():
     rnd, cfg = sys.argv[1], sys.argv[2]
     inst = int(sys.argv[3]) if len(sys.argv) > 3 else {"c2": 65536, "c3": 1 << 20}[cfg]
-    src = os.path.join(ROOT, "gpurun_out", f"pmc_{cfg}")
+    src = os.path.join(ROOT, "gpurun_out", f"pmc_{cfg}" + (sys.argv[6] if len(sys.argv) > 6 else ""))
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     stats = os.path.join(src, "trace", "p_kernel_stats.csv")
