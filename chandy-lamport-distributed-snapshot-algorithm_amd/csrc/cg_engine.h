@@ -124,6 +124,10 @@ struct GScal {
   unsigned long long sg_draw0;   // the group's first draw index
   // partitioned mode: this device's tick totals (k_scan), global bases set by the host
   unsigned long long tot_trig, tot_send;
+  // draws of the last tick whose k_push scanned its own bases (small graphs, no k_scan):
+  // folded into `draw` by the next kernel that reads it (fold_draw), since every k_push block
+  // reads `draw` while the tick runs
+  unsigned long long draw_pend;
 };
 enum : int32_t { kDrainWait = 0, kDrainExtra = 1, kDrainDone = 2, kDrainHang = 3 };
 constexpr int32_t kTimeFromDevice = -1;  // tick argument -1 - k: drain slot k (time, skip in GScal)

@@ -87,6 +87,16 @@ __device__ inline int32_t tick_time(const GParams& p, int32_t targ) {
 
 __device__ inline void set_status(GScal* sc, int32_t code) { atomicCAS(&sc->status, 0, code); }
 
+// The draw counter after a tick whose k_push scanned its own bases (GScal::draw_pend): one
+// thread of the next kernel that reads `draw` folds the pending count in first.
+__device__ inline void fold_draw(GScal* sc) {
+  const unsigned long long d = sc->draw_pend;
+  if (d) {
+    sc->draw += d;
+    sc->draw_pend = 0;
+  }
+}
+
 // Append one Logger record (trace runs only; one device counter: a debugging aid for
 // graphs of modest size).
 __device__ inline void gtrace(const GParams& p, int32_t epoch, uint32_t part, uint32_t key, uint32_t sub, int32_t kind,
@@ -342,6 +352,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
   __shared__ uint64_t s_hq[kStage];
   const int bk = p.blk_lo + (int)blockIdx.x;  // (the owned blocks in the partitioned mode)
   const int s = bk * kGThreads + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) fold_draw(p.sc);  // (the previous tick's draws)
   const int32_t blo = p.out_off[bk * kGThreads];
   const int32_t bhi = p.out_off[min((bk + 1) * kGThreads, p.n)];
   const int32_t nst = min(bhi - blo, kStage);
@@ -613,6 +624,7 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t 
     p.sc->tot_trig = (unsigned long long)carry_a;
     p.sc->tot_send = (unsigned long long)carry_b;
   } else if (threadIdx.x == 0) {
+    fold_draw(p.sc);
     const unsigned long long d = p.sc->draw;
     p.sc->base_trig = d;
     p.sc->base_send = d + (unsigned long long)carry_a;
@@ -630,6 +642,18 @@ __device__ inline uint64_t next_creation(const GParams& p, int32_t lo, int ncre,
     if ((r == 0 || x > prev) && x < best) best = x;
   }
   return best;
+}
+
+// A tick's draw bases for k_push: the trigger and send bases and the exclusive block
+// prefixes [2 * block] (triggers) / [2 * block + 1] (sends) -- k_scan's (GScal, bsum), or the
+// ones a small graph's k_push scans itself into LDS.
+struct Bases {
+  unsigned long long trig, send;
+  const long long* pre;
+};
+__device__ inline unsigned long long bdraw(const GParams& p, const Bases& b, int32_t s0) {
+  if (s0 < p.part_lo || s0 >= p.part_hi) return p.rdraw[s0];  // partitioned: the sender's device replied
+  return b.trig + (unsigned long long)b.pre[2 * (s0 / kGThreads)] + (unsigned long long)p.ltrig[s0];
 }
 
 // First draw index of the broadcast triggered by sender s0's delivery this tick, and of
@@ -664,8 +688,8 @@ __device__ inline void push_q(const GParams& p, int32_t c, uint64_t& q, uint32_t
 // reference's (queue.go:18-20); draw indices are the absolute out-link positions.
 constexpr int kRegOd = 8;
 template <int R>
-__device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int32_t ob, int32_t od, int ncre,
-                                     bool send, int32_t tok, int32_t tj, unsigned long long sd,
+__device__ inline void push_node_reg(const GParams& p, const Bases& bs, int32_t t, int32_t v, int32_t ob, int32_t od,
+                                     int ncre, bool send, int32_t tok, int32_t tj, unsigned long long sd,
                                      unsigned long long (&c)[2]) {
   p.crn[v] = 0;
   const int32_t lo = p.in_off[v];
@@ -695,7 +719,7 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
         for (int j = 0; j < R; ++j)
           if (j < m && j0 + j < pj && (uint32_t)q[j] == kEmpty) ++c[1];
       }
-      const unsigned long long draw0 = broadcast_draw(p, s0) + (unsigned long long)j0;
+      const unsigned long long draw0 = bdraw(p, bs, s0) + (unsigned long long)j0;
 #pragma unroll
       for (int j = 0; j < R; ++j)
         if (j < m) push_q(p, obc + j, q[j], kGMarker | sid, receive_time(p, draw0 + j, t), c[0]);
@@ -720,8 +744,8 @@ __device__ inline void push_node_reg(const GParams& p, int32_t t, int32_t v, int
 // node's broadcasts in creating-sender order, then the traffic send (queue.go:18-20), so
 // per-channel FIFO order is the same as one thread pushing them all.
 template <int L>
-__device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, int32_t ob, int32_t od, int ncre,
-                                       bool send, int32_t tok, int32_t tj, unsigned long long sd, int32_t jl,
+__device__ inline void push_node_lanes(const GParams& p, const Bases& bs, int32_t t, int32_t v, int32_t ob, int32_t od,
+                                       int ncre, bool send, int32_t tok, int32_t tj, unsigned long long sd, int32_t jl,
                                        unsigned long long (&c)[2]) {
   if (jl == 0) {
     p.crn[v] = 0;
@@ -742,7 +766,7 @@ __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, i
         const int pj = (pk >> 6) == t ? (pk & 63) : 64;
         if (j < pj && (uint32_t)q == kEmpty) ++c[1];
       }
-      push_q(p, ob + j, q, kGMarker | sid, receive_time(p, broadcast_draw(p, s0) + (unsigned long long)j, t), c[0]);
+      push_q(p, ob + j, q, kGMarker | sid, receive_time(p, bdraw(p, bs, s0) + (unsigned long long)j, t), c[0]);
     }
     if (send && j == tj) {
       push_q(p, ob + j, q, 1u, receive_time(p, sd, t), c[0]);
@@ -755,8 +779,14 @@ __device__ inline void push_node_lanes(const GParams& p, int32_t t, int32_t v, i
 // phase D: every node pushes onto its own out-channels -- the broadcasts of the local
 // snapshots created at it this tick (in creating-sender order), then its traffic send;
 // then the grid expands the local snapshots created at high in-degree nodes.
-template <int L>
-__global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int32_t sarg) {
+// FUSED (graphs of at most kFuseBlocks node blocks, C5): no k_scan launch -- every block
+// scans the block tallies itself (2 per thread, L2-resident) into LDS, block 0 leaves the
+// tick's draw count in GScal::draw_pend and makes k_scan's drain decision for the next tick
+// (completions all happened in k_marker).
+constexpr int32_t kFuseBlocks = 2 * kGThreads;
+template <int L, bool FUSED>
+__global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int32_t sarg, int32_t n_before,
+                                                    int32_t max_drain) {
   const int32_t t = tick_time(p, targ);
   const int32_t step = sarg >= 0 ? sarg : t;  // the traffic of step t follows tick t
   const int64_t gid = ((int64_t)p.blk_lo * kGThreads * L) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -774,16 +804,63 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
     // block tally) and, for a node without broadcasts, the channel's head word
     send = traffic_send(p, step, v, od, tok, &tj);
     if (send) {
-      sd = send_draw(p, v);
+      if (!FUSED) sd = send_draw(p, v);
       if (jl == 0) q0 = p.hq[ob + tj];
     }
   }
-  if (block_frozen(p, targ)) return;
+  long long ta0 = 0, tb0 = 0, ta1 = 0, tb1 = 0;  // (FUSED) this thread's two block tallies
+  if constexpr (FUSED) {
+    const int32_t i0 = 2 * (int32_t)threadIdx.x;
+    if (i0 < p.n_pblocks) {
+      ta0 = p.bsum[2 * i0];
+      tb0 = p.bsum[2 * i0 + 1];
+    }
+    if (i0 + 1 < p.n_pblocks) {
+      ta1 = p.bsum[2 * i0 + 2];
+      tb1 = p.bsum[2 * i0 + 3];
+    }
+  }
+  if (block_frozen(p, targ)) {
+    if (FUSED && targ < 0 && blockIdx.x == 0 && threadIdx.x == 0)
+      drain_decide(p, n_before, max_drain, (-1 - targ) ^ 1);  // (stays frozen)
+    return;
+  }
+  Bases bs{0ull, 0ull, p.bsum};
+  __shared__ long long s_pre[FUSED ? 2 * kFuseBlocks : 2];
+  __shared__ unsigned long long s_base[2];
+  if constexpr (FUSED) {
+    __shared__ long long s_sh[2 * (kGThreads / 64)];
+    const int32_t i0 = 2 * (int32_t)threadIdx.x;
+    long long a = ta0 + ta1, b = tb0 + tb1, tot_a, tot_b;
+    block_exclusive_scan2(a, b, tot_a, tot_b, s_sh);
+    if (i0 < p.n_pblocks) {
+      s_pre[2 * i0] = a;
+      s_pre[2 * i0 + 1] = b;
+    }
+    if (i0 + 1 < p.n_pblocks) {
+      s_pre[2 * i0 + 2] = a + ta0;
+      s_pre[2 * i0 + 3] = b + tb0;
+    }
+    if (threadIdx.x == 0) {
+      const unsigned long long d = p.sc->draw;  // (folded by this tick's k_pick)
+      s_base[0] = d;
+      s_base[1] = d + (unsigned long long)tot_a;
+      if (blockIdx.x == 0) {
+        p.sc->draw_pend = (unsigned long long)(tot_a + tot_b);
+        if (targ < 0) drain_decide(p, n_before, max_drain, (-1 - targ) ^ 1);  // the next drain tick
+      }
+    }
+    __syncthreads();
+    bs = Bases{s_base[0], s_base[1], s_pre};
+    if (send) sd = bs.send + (unsigned long long)s_pre[2 * (v / kGThreads) + 1] + (unsigned long long)p.lsend[v];
+  } else {
+    bs = Bases{p.sc->base_trig, p.sc->base_send, p.bsum};
+  }
   unsigned long long c[2] = {0, 0};  // push, peek
   if (v < p.part_hi) {
     if (ncre) {
-      if constexpr (L == 1) push_node_reg<kRegOd>(p, t, v, ob, od, ncre, send, tok, tj, sd, c);
-      else push_node_lanes<L>(p, t, v, ob, od, ncre, send, tok, tj, sd, jl, c);
+      if constexpr (L == 1) push_node_reg<kRegOd>(p, bs, t, v, ob, od, ncre, send, tok, tj, sd, c);
+      else push_node_lanes<L>(p, bs, t, v, ob, od, ncre, send, tok, tj, sd, jl, c);
     } else if (send && jl == 0) {
       // SendTokens(v, out-link j, 1): node.go:112-131 (one channel: no batching)
       p.tokens[v] = tok - 1;
@@ -844,6 +921,7 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
   __shared__ int s_stop;
   __shared__ unsigned long long s_draw;
   unsigned long long pushes = 0;
+  if (threadIdx.x == 0) fold_draw(p.sc);  // (ordered before the loop's first barrier)
   for (int i = 0; i < oc; ++i) {
     const GOp op = p.ops[ob + i];
     // (an L2 read: other threads' pushes may have set the status with an atomic)
@@ -1061,6 +1139,7 @@ __global__ void k_bk_bases(GParams p) {
     if (!p.sc->status) p.sc->status = (int32_t)st;
     return;
   }
+  fold_draw(p.sc);
   const unsigned long long d = p.sc->draw;
   p.sc->base_trig = d + (unsigned long long)tb;
   p.sc->base_send = d + (unsigned long long)(ta + sb);
@@ -1101,6 +1180,7 @@ __global__ void __launch_bounds__(kGThreads) k_part_trig(GParams p, const int2* 
 // device's; the next step's sends likewise after every trigger (sim.go:101 call order).
 __global__ void k_part_bases(GParams p, long long trig_before, long long trig_all, long long send_before,
                              long long send_all) {
+  fold_draw(p.sc);
   const unsigned long long d = p.sc->draw;
   p.sc->base_trig = d + (unsigned long long)trig_before;
   p.sc->base_send = d + (unsigned long long)(trig_all + send_before);
@@ -1223,17 +1303,28 @@ void launch_pick(const GParams& p, dim3 grid, int32_t t, hipStream_t s) {
 // (cl_graph_set_push_lanes: the exact-match tests run both on the same graphs).
 constexpr int32_t kLanesBelow = 1 << 18;
 // (over the owned node blocks [blk_lo, blk_hi): all of them outside the partitioned mode)
-void launch_push(const GParams& p, int32_t t, int32_t step, hipStream_t s) {
+// fused: k_push scans the tick's draw bases itself (no k_scan launch; fuse_scan(p)).
+template <bool F>
+static void launch_push_t(const GParams& p, int32_t t, int32_t step, hipStream_t s, int32_t n_before, int32_t md) {
   const int32_t nb = p.blk_hi - p.blk_lo;
   if (nb <= 0) return;
   if (p.push_lanes ? p.push_lanes == kPushLanes : p.n < kLanesBelow) {
     const int64_t m = (int64_t)(p.part_hi - p.part_lo) * kPushLanes;
-    hipLaunchKernelGGL(k_push<kPushLanes>, dim3((unsigned)((m + kGThreads - 1) / kGThreads)), dim3(kGThreads), 0, s, p, t, step);
+    hipLaunchKernelGGL((k_push<kPushLanes, F>), dim3((unsigned)((m + kGThreads - 1) / kGThreads)), dim3(kGThreads), 0, s,
+                       p, t, step, n_before, md);
   } else {
-    hipLaunchKernelGGL(k_push<1>, dim3(nb), dim3(kGThreads), 0, s, p, t, step);
+    hipLaunchKernelGGL((k_push<1, F>), dim3(nb), dim3(kGThreads), 0, s, p, t, step, n_before, md);
   }
 }
+void launch_push(const GParams& p, int32_t t, int32_t step, hipStream_t s) { launch_push_t<false>(p, t, step, s, 0, 0); }
 void launch_push(const GParams& p, int32_t t, hipStream_t s) { launch_push(p, t, t, s); }
+// Small whole-graph runs fold the scan into k_push (C5: 391 node blocks; one launch and its
+// boundary less per tick); large ones keep k_scan (C4: 4,096 tallies per block would be
+// 64 KB of L2 reads per k_push block).
+#ifndef CLSNAP_FUSE_SCAN
+#define CLSNAP_FUSE_SCAN 1
+#endif
+static bool fuse_scan(const GParams& p) { return CLSNAP_FUSE_SCAN && !p.part && p.n_pblocks <= kFuseBlocks; }
 
 // k_scan on a per-tick latency path: up to 512 block tallies (C5: 391) are scanned by one
 // wave, eight per thread; more by whole waves of four per thread, at most 1024 threads
@@ -1260,8 +1351,12 @@ int cg_launch_tick(const GParams& p, int32_t t, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   launch_pick(p, dim3(p.n_pblocks), t, s);
   hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, t);
-  launch_scan(p, t, 0, 0, s);
-  launch_push(p, t, s);
+  if (fuse_scan(p)) {
+    launch_push_t<true>(p, t, t, s, 0, 0);
+  } else {
+    launch_scan(p, t, 0, 0, s);
+    launch_push(p, t, s);
+  }
   return hipGetLastError();
 }
 
@@ -1281,8 +1376,12 @@ int cg_launch_drain_ticks(const GParams& p, int32_t n_before, int64_t max_drain,
     const int32_t ta = -1 - (int32_t)((first + i) & 1);
     launch_pick(p, dim3(p.n_pblocks), ta, s);
     hipLaunchKernelGGL(k_marker<false>, dim3(p.n_pblocks), dim3(kGThreads), 0, s, p, ta);
-    launch_scan(p, ta, n_before, md, s);
-    launch_push(p, ta, ta, s);
+    if (fuse_scan(p)) {
+      launch_push_t<true>(p, ta, ta, s, n_before, md);
+    } else {
+      launch_scan(p, ta, n_before, md, s);
+      launch_push(p, ta, ta, s);
+    }
   }
   return hipGetLastError();
 }
@@ -1298,6 +1397,7 @@ int cg_launch_hostops(const GParams& p, int32_t time, int32_t op_begin, int32_t 
 }
 
 __global__ void k_sg_begin(GParams p) {
+  fold_draw(p.sc);
   p.sc->sg_first = 0x7fffffff;
   p.sc->sg_frozen = p.sc->status;
 }

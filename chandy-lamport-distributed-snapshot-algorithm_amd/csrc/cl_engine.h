@@ -283,6 +283,10 @@ struct ExecLaunch {
   void* stream2;  // split replays: the spill-capable part runs here (fork / join events)
   void* ev_fork;
   void* ev_join;
+  // split replays back to back (cl_host.cpp): fork = stream2 first waits for the engine
+  // stream (new work there since the last fork), join = the engine stream waits for stream2
+  // before the stop event (else the join is deferred to the next call that is not a rerun)
+  int32_t fork, join;
 };
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
 int launch_checksums(const SumParams& p, void* stream);

@@ -55,6 +55,9 @@ constexpr int32_t kTargetBlocks = 6;
 // Batches of at least this many instances replay through a length-ordered slot map (a few
 // thousand waves: the grouping pays for its one host sort and 4 B per instance of HBM).
 constexpr int64_t kMapMinInstances = 4096;
+#ifndef CLSNAP_PIPE
+#define CLSNAP_PIPE 2  // split replays back to back: 0 join every replay, 1 neither fork nor join, 2 fork only (A/B knob)
+#endif
 #ifndef CLSNAP_LPT
 #define CLSNAP_LPT 1  // slot map order: 1 longest instances first, 0 shortest first (A/B knob)
 #endif
@@ -297,6 +300,22 @@ struct cl_sim {
   int64_t plan_split = 0, plan_spilled = 0;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // Split replays back to back (CLSNAP_PIPE): the spill-capable half of a replay on stream2
+  // and the spill-free half on `stream` touch disjoint instances, so consecutive replays need
+  // no cross-stream wait between them -- a replay's halves overlap the previous replay's
+  // tail.  s2_live: stream2 may hold work `stream` has not waited for; every other ABI call
+  // joins it first (join_stream2, SIM_CHECK).  s_dirty: `stream` got work since the last
+  // fork, so the next replay's stream2 half must wait for it.
+  bool s2_live = false, s_dirty = true;
+  int join_stream2() {
+    s_dirty = true;
+    if (!s2_live) return CL_OK;
+    s2_live = false;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipEventRecord(ev_join, stream2));
+    HIP_TRY(hipStreamWaitEvent(stream, ev_join, 0));
+    return CL_OK;
+  }
   // wave end their drains together; replays of the same program and delays launch through
   // the map (results are per instance, unchanged).  -1: no map.
   DevBuf<int32_t> d_map;
@@ -325,6 +344,7 @@ struct cl_sim {
   ~cl_sim() {
     if (dev_ready) {
       (void)hipSetDevice(device);
+      if (stream2) (void)hipStreamSynchronize(stream2);
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
@@ -696,7 +716,15 @@ struct cl_sim {
     // the dispatch records both events (the kernel's own start/end timestamps): two
     // hipEventRecord packets around it cost 0.7 us more per launch (C2 0.1816 -> 0.1809 ms per
     // step) and bracketed ~1 us of packet processing into the kernel time
-    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p, ExecLaunch{stream, pr.first, pr.second, stream2, ev_fork, ev_join});
+    const bool pipe = CLSNAP_PIPE && planned && p.split_slot > 0 && p.split_slot < n_inst && stream2 && !save_state;
+    if (!pipe && (rc = join_stream2())) return rc;
+    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p,
+                        ExecLaunch{stream, pr.first, pr.second, stream2, ev_fork, ev_join,
+                                   pipe && CLSNAP_PIPE == 1 ? (s_dirty ? 1 : 0) : 1, pipe ? 0 : 1});
+    if (pipe) {
+      s2_live = true;
+      s_dirty = false;
+    }
     if (e != 0) return set_err(CL_E_DEVICE, "exec kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     ev0 = pr.first;
     ev1 = pr.second;
@@ -959,9 +987,16 @@ const char* cl_status_string(int32_t code) {
   }
 }
 
-#define SIM_CHECK(s)                                                \
+// Every ABI call but cl_rerun first joins a pipelined replay's stream2 half (cl_sim::s2_live).
+#define SIM_CHECK_NOJOIN(s)                                         \
   if (!(s)) return set_err(CL_E_INVALID, "null cl_sim handle");  \
   std::lock_guard<std::recursive_mutex> sim_lock_((s)->mu)
+#define SIM_CHECK(s)                                                \
+  SIM_CHECK_NOJOIN(s);                                              \
+  if ((s)->s2_live) {                                               \
+    const int jrc_ = const_cast<cl_sim*>(s)->join_stream2();        \
+    if (jrc_) return jrc_;                                          \
+  }
 
 int cl_sim_create(int64_t n_instances, cl_sim** out) {
   if (!out || n_instances <= 0) return set_err(CL_E_INVALID, "n_instances must be > 0");
@@ -1207,7 +1242,7 @@ int cl_flush(cl_sim* sim) {
 }
 
 int cl_rerun(cl_sim* sim) {
-  SIM_CHECK(sim);
+  SIM_CHECK_NOJOIN(sim);
   return sim->launch(true, false);
 }
 

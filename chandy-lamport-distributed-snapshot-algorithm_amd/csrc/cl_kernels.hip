@@ -1061,7 +1061,8 @@ int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, 
                       const ExecLaunch& L) {
   hipStream_t s = (hipStream_t)L.stream, s2 = (hipStream_t)L.stream2;
   hipError_t he;
-  if ((he = hipEventRecord((hipEvent_t)L.ev_fork, s)) || (he = hipStreamWaitEvent(s2, (hipEvent_t)L.ev_fork, 0)))
+  if (L.fork &&
+      ((he = hipEventRecord((hipEvent_t)L.ev_fork, s)) || (he = hipStreamWaitEvent(s2, (hipEvent_t)L.ev_fork, 0))))
     return (int)he;
   ExecParams a = p, b = p;
   a.n_inst = p.split_slot;
@@ -1081,6 +1082,10 @@ int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, 
   } else {
     if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
     if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, L, s2))) return e;
+  }
+  if (!L.join) {  // replays back to back: the main stream does not wait for stream2 (cl_host.cpp)
+    if (L.ev_stop && (he = hipEventRecord((hipEvent_t)L.ev_stop, s))) return (int)he;
+    return 0;
   }
   if ((he = hipEventRecord((hipEvent_t)L.ev_join, s2)) || (he = hipStreamWaitEvent(s, (hipEvent_t)L.ev_join, 0)))
     return (int)he;

@@ -135,7 +135,10 @@ int cl_read_events_text(cl_sim* sim, const char* text, int32_t* n_snapshots);
 /* Execute pending events on the GPU and wait. */
 int cl_flush(cl_sim* sim);
 /* Re-run the whole event program from the initial topology state (asynchronous on
- * the sim's stream; inputs stay resident in HBM).  cl_synchronize() waits. */
+ * the sim's stream; inputs stay resident in HBM).  cl_synchronize() waits.  A replay split
+ * over two streams (cl_replay_split) leaves its spill-capable half running when the call
+ * returns: back-to-back cl_rerun calls overlap that half with the next replay's spill-free
+ * half (they touch disjoint instances); every other call waits for it first. */
 int cl_rerun(cl_sim* sim);
 int cl_synchronize(cl_sim* sim);
 /* Device time of the most recent cl_flush/cl_rerun kernel, from HIP events on the
