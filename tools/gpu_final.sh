@@ -3,8 +3,9 @@
 #   PART=bench  bench lines: c3 (default, with cpu_baseline), c3 at the per-GPU share of an
 #               8-GPU node (2^17 instances), c2, c4 and c5 (with their cpu baselines), and a
 #               2-rank gloo rehearsal of the multi-GPU path on one card
-#   PART=prof   exec-kernel PMC + kernel stats (c3, c3 at 2^17, c2); graph kernel stats
-#               (c4, c5) and graph HBM traffic (c4, c5 with the drain)
+#   PART=prof   exec-kernel PMC + kernel stats (c3, c3 at 2^17, c2: tools/make_profiles.py
+#               turns gpurun_out/pmc_* into profiles/); graph kernel stats (c4, c5) and graph
+#               HBM traffic (c4, c5 with the drain), summarised on the box
 # usage: TAG=r03f PART=bench bash tools/gpu_final.sh
 set -e
 R=$GRAFT_REPO_ROOT
@@ -24,6 +25,10 @@ else
   CFG=c2 bash tools/gpu_pmc.sh
   CFG=c4 ARGS="--steps 3 --warmup 1" bash tools/gpu_prof_graph.sh
   CFG=c5 ARGS="--steps 1 --warmup 1" bash tools/gpu_prof_graph.sh
-  CFG=c4 bash tools/gpu_pmc_graph.sh
-  CFG=c5 bash tools/gpu_pmc_graph.sh
+  # (the graph passes' per-dispatch CSVs stay in /tmp on the box: C5 has ~10^6 dispatches;
+  # only the traffic summaries come back, under $O/profiles)
+  PMCG_ROOT=/tmp CFG=c4 bash tools/gpu_pmc_graph.sh
+  PMCG_DIR=/tmp/pmcg_c4 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c4 1048576 80 > $O/traffic_c4.log
+  PMCG_ROOT=/tmp CFG=c5 bash tools/gpu_pmc_graph.sh
+  PMCG_DIR=/tmp/pmcg_c5 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c5 100000 4100 drain > $O/traffic_c5.log
 fi

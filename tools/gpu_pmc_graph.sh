@@ -3,7 +3,7 @@
 # usage: CFG=c4|c5 bash tools/gpu_pmc_graph.sh   -> gpurun_out/pmcg_<cfg>/pass{3,4}/
 set -e
 CFG=${CFG:-c4}
-OUT=$GRAFT_REPO_ROOT/gpurun_out/pmcg_$CFG
+OUT=${PMCG_ROOT:-$GRAFT_REPO_ROOT/gpurun_out}/pmcg_$CFG
 rm -rf $OUT; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 P=$GRAFT_REPO_ROOT/bench.py

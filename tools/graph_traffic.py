@@ -1,6 +1,7 @@
 """HBM bytes per graph-engine run from the gpu_pmc_graph.sh passes -> profiles/traffic_<cfg>.json.
 
 usage: python tools/graph_traffic.py <cfg> <nodes> <ticks> [drain]
+(env PMCG_DIR: the passes' directory, default gpurun_out/pmcg_<cfg>; OUT_DIR: default profiles/)
 A run is k_reset + the tick kernels (k_hostops, k_tally, k_pick, k_marker, k_scan, k_push);
 the post-run checks (k_finish, k_checks_*) are excluded.  Runs = k_reset dispatches.
 Bytes follow MI355X_MICROARCH.md's gfx950 correction as tools/make_profiles.py does:
@@ -35,7 +36,7 @@ def sums(pattern):
 
 
 cfg, nodes, ticks = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-base = os.path.join(ROOT, "gpurun_out", f"pmcg_{cfg}")
+base = os.environ.get("PMCG_DIR") or os.path.join(ROOT, "gpurun_out", f"pmcg_{cfg}")
 drain = len(sys.argv) > 4 and sys.argv[4] == "drain"
 f, runs_f, fk = sums(os.path.join(base, "pass3", "**", "*counter_collection.csv"))
 w, runs_w, wk = sums(os.path.join(base, "pass4", "**", "*counter_collection.csv"))
@@ -49,5 +50,7 @@ out = {"config": cfg, "nodes": nodes, "steps": ticks, "drain": drain, "runs_prof
        "per_kernel_fetch_kb_per_run": {k: fk[k] / runs_f for k in sorted(fk)},
        "per_kernel_write_kb_per_run": {k: wk[k] / runs_w for k in sorted(wk)},
        "note": "one launch = one full run of the tick pipeline; (2*FETCH_SIZE + WRITE_SIZE) KB per gfx950 correction"}
-json.dump(out, open(os.path.join(ROOT, "profiles", f"traffic_{cfg}.json"), "w"), indent=1)
+out_dir = os.environ.get("OUT_DIR") or os.path.join(ROOT, "profiles")
+os.makedirs(out_dir, exist_ok=True)
+json.dump(out, open(os.path.join(out_dir, f"traffic_{cfg}.json"), "w"), indent=1)
 print(json.dumps(out))

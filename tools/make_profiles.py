@@ -35,7 +35,7 @@ def main():
     rnd, cfg = sys.argv[1], sys.argv[2]
     inst = int(sys.argv[3]) if len(sys.argv) > 3 else {"c2": 65536, "c3": 1 << 20}[cfg]
     src = os.path.join(ROOT, "gpurun_out", f"pmc_{cfg}" + (sys.argv[6] if len(sys.argv) > 6 else ""))
-    out = os.path.join(ROOT, "profiles")
+    out = os.environ.get("OUT_DIR") or os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     stats = os.path.join(src, "trace", "p_kernel_stats.csv")
     shutil.copy(stats, os.path.join(out, f"{rnd}_{cfg}_kernel_stats.csv"))
