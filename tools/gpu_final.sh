@@ -11,7 +11,13 @@ set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${TAG:-final}
 mkdir -p $O
-if [ "${PART:-bench}" = bench ]; then
+if [ "${PART:-bench}" = c5traffic ]; then
+  ( while true; do date >> $O/heartbeat.log; sleep 30; done ) &
+  HB=$!
+  PASS_S=540 PMCG_ROOT=/tmp CFG=c5 bash tools/gpu_pmc_graph.sh || { kill $HB; exit 1; }
+  kill $HB
+  PMCG_DIR=/tmp/pmcg_c5 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c5 100000 4100 drain > $O/traffic_c5.log
+elif [ "${PART:-bench}" = bench ]; then
   timeout -k 10 300 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.err
   timeout -k 10 300 python -u bench.py --instances 131072 --no-cpu-baseline > $O/bench_c3_s17.json 2> $O/bench_c3_s17.err
   timeout -k 10 300 python -u bench.py --config c2 --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err
@@ -29,6 +35,10 @@ else
   # only the traffic summaries come back, under $O/profiles)
   PMCG_ROOT=/tmp CFG=c4 bash tools/gpu_pmc_graph.sh
   PMCG_DIR=/tmp/pmcg_c4 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c4 1048576 80 > $O/traffic_c4.log
-  PMCG_ROOT=/tmp CFG=c5 bash tools/gpu_pmc_graph.sh
+  # C5's passes write nothing for minutes: a heartbeat file keeps the run visibly alive
+  ( while true; do date >> $O/heartbeat.log; sleep 30; done ) &
+  HB=$!
+  PASS_S=540 PMCG_ROOT=/tmp CFG=c5 bash tools/gpu_pmc_graph.sh || { kill $HB; exit 1; }
+  kill $HB
   PMCG_DIR=/tmp/pmcg_c5 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c5 100000 4100 drain > $O/traffic_c5.log
 fi
