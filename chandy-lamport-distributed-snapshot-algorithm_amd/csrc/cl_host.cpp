@@ -58,6 +58,9 @@ constexpr int64_t kMapMinInstances = 4096;
 #ifndef CLSNAP_PIPE
 #define CLSNAP_PIPE 2  // split replays back to back: 0 join every replay, 1 neither fork nor join, 2 fork only (A/B knob)
 #endif
+#ifndef CLSNAP_MAP_PCT
+#define CLSNAP_MAP_PCT 92  // length-ordered slot map when it keeps at most this % of the wave-ticks (A/B knob)
+#endif
 #ifndef CLSNAP_LPT
 #define CLSNAP_LPT 1  // slot map order: 1 longest instances first, 0 shortest first (A/B knob)
 #endif
@@ -800,7 +803,7 @@ struct cl_sim {
     // worth it only when it removes enough wave-ticks to pay for the scattered stores (C3:
     // 43.9 -> 39.5 ticks per wave, kept; C2: 55.8 -> 52.8, measured slower mapped)
     const int64_t nc = (int64_t)clean.size();
-    const bool sort = n_inst >= kMapMinInstances && wave_ticks(t, by_len, 0, nc) * 100 <= wave_ticks(t, clean, 0, nc) * 92;
+    const bool sort = n_inst >= kMapMinInstances && wave_ticks(t, by_len, 0, nc) * 100 <= wave_ticks(t, clean, 0, nc) * CLSNAP_MAP_PCT;
     std::vector<int32_t> order = sort ? by_len : clean;
     order.insert(order.end(), spilled.begin(), spilled.end());
     const int64_t ipw = std::max(lay.ipw, 1);

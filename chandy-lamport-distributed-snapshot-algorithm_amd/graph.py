@@ -352,6 +352,20 @@ class GraphSim:
         return format_log(self.node_ids(), self.trace())
 
 
+def bucket_capacity(src, dst, span, world):
+    """Rows per device-exchange bucket of the partitioned mode: the most nodes of one rank
+    with a channel into another rank's nodes (rank r owns node ranks [r * span, (r + 1) *
+    span)).  Each sender delivers at most one packet per tick (sim.go:90), so this bounds
+    the deliveries from r to q, the broadcast reports q sends r about r's senders, and r's
+    replies to them."""
+    w = world
+    key = np.unique(np.asarray(src, dtype=np.int64) * w + np.asarray(dst, dtype=np.int64) // span)
+    pair = (key // w) // span * w + key % w
+    cnt = np.bincount(pair, minlength=w * w).reshape(w, w)
+    np.fill_diagonal(cnt, 0)
+    return max(int(cnt.max()), 1)
+
+
 class PartitionedGraphSim:
     """ONE simulation over a graph split into contiguous node-rank ranges, one range per
     process / GPU (graph-partitioned mode, DESIGN.md §11, include/clgraph.h
@@ -396,16 +410,9 @@ class PartitionedGraphSim:
 
     # ---- device-resident exchange (clgraph.h cl_graph_part_dev_*) ----------------------
     def bucket_capacity(self):
-        """Rows per exchange bucket: the most nodes of one rank with a channel into another
-        rank's nodes -- each sender delivers at most one packet per tick, so this bounds the
-        deliveries, the broadcast reports and the replies between any two ranks."""
+        """Rows per exchange bucket for this graph and rank split (bucket_capacity below)."""
         src, dst = self.g.channels()
-        w = self.world
-        key = np.unique(src.astype(np.int64) * w + dst.astype(np.int64) // self.span)
-        pair = (key // w) // self.span * w + key % w
-        cnt = np.bincount(pair, minlength=w * w).reshape(w, w)
-        np.fill_diagonal(cnt, 0)
-        return max(int(cnt.max()), 1)
+        return bucket_capacity(src, dst, self.span, self.world)
 
     def _dev_setup(self):
         import torch
