@@ -803,13 +803,17 @@ struct cl_sim {
     // worth it only when it removes enough wave-ticks to pay for the scattered stores (C3:
     // 43.9 -> 39.5 ticks per wave, kept; C2: 55.8 -> 52.8, measured slower mapped)
     const int64_t nc = (int64_t)clean.size();
-    const bool sort = n_inst >= kMapMinInstances && wave_ticks(t, by_len, 0, nc) * 100 <= wave_ticks(t, clean, 0, nc) * CLSNAP_MAP_PCT;
-    std::vector<int32_t> order = sort ? by_len : clean;
-    order.insert(order.end(), spilled.begin(), spilled.end());
     const int64_t ipw = std::max(lay.ipw, 1);
     // split replays: the clean instances' whole waves on the spill-free kernel (a wave that
     // holds a spilling instance runs spill-capable), when the launcher's kernels can split
-    if (!spilled.empty() && specialized()) plan_split = nc / ipw * ipw;
+    const bool split = !spilled.empty() && specialized();
+    // a split launches through the map anyway (its scattered result stores are paid), so the
+    // clean instances then go in length order too (C2: 0.1829 -> 0.1807 ms per step)
+    const bool sort = n_inst >= kMapMinInstances &&
+                      (split || wave_ticks(t, by_len, 0, nc) * 100 <= wave_ticks(t, clean, 0, nc) * CLSNAP_MAP_PCT);
+    std::vector<int32_t> order = sort ? by_len : clean;
+    order.insert(order.end(), spilled.begin(), spilled.end());
+    if (split) plan_split = nc / ipw * ipw;
     plan_map = sort || plan_split > 0;
     if (plan_map) {
       int rc = d_map.ensure(order.size());
