@@ -70,6 +70,7 @@ struct Ctx {
   // snapshot outputs by 32-bit byte offsets from the (uniform) array bases: the stores use
   // the SGPR-base + 32-bit-VGPR-offset form, with no 64-bit address arithmetic per store
   uint32_t nod_plane;  // bytes per sid plane of the node records (uniform)
+  int32_t draws;       // delays per instance, clamped to int32 (draw indices are int32)
   bool mul24;  // every plane offset sid * plane fits the 24-bit multiplier
 };
 
@@ -194,9 +195,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // the compiler waits with s_waitcnt vmcnt(0) at the join, and on gfx950 vmcnt also counts
 // the wave's outstanding global STORES (snapshot outputs) -- a full store drain per push.
 template <bool STAGED>
-__device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int64_t k) {
+__device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int32_t k) {
   const Layout& lay = x.lay;
-  if (k >= x.p.draws) { ln.flag = ST_DELAY_EXHAUSTED; return; }
+  if (k >= x.draws) { ln.flag = ST_DELAY_EXHAUSTED; return; }
   const uint32_t chw = CHW(ko);
   const uint32_t cnt = chw >> 8;
   if (cnt >= (uint32_t)kMaxQueued) { ln.flag = ST_FIFO_OVERFLOW; return; }
@@ -456,7 +457,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       const uint32_t src = tv & 0xffu;
       const uint32_t sid = tv >> 8;
       // exclusive prefix of the triggering sender within the instance
-      const int64_t k0 = (int64_t)ln.draw + (XW(lay.x_off + x.seg_base + src) - (uint32_t)x.outdeg - base);
+      const int32_t k0 = ln.draw + (int32_t)(XW(lay.x_off + x.seg_base + src) - (uint32_t)x.outdeg - base);
 #pragma unroll
       for (int32_t j = 0; j < D; ++j) {
         if (j >= x.outdeg) continue;
@@ -529,7 +530,7 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
   const bool mine = ln.alive && pos >= 0;
   bool bad = false;
   if (mine) {
-    if (ln.tokens < on || oj < 0 || (int64_t)ln.draw + pos >= x.p.draws) {
+    if (ln.tokens < on || oj < 0 || ln.draw + pos >= x.draws) {
       bad = true;
     } else {  // the checks push() makes
       const uint32_t cnt = (uint32_t)CHW(oj) >> 8, cap = 1u << lay.cap_log2;
@@ -546,7 +547,7 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
     ln.tokens -= on;
 #pragma unroll
     for (int32_t j = 0; j < D; ++j)
-      if (j == oj) push<STAGED>(x, ln, j, (uint32_t)on, (int64_t)ln.draw + pos);
+      if (j == oj) push<STAGED>(x, ln, j, (uint32_t)on, ln.draw + pos);
   }
   if (ln.alive) ln.draw += k;
 }
@@ -619,6 +620,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   const Ctx x{p, lay, X + lay.col + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0,
               4u * st * (uint32_t)N * (uint32_t)lay.rw,
+              (int32_t)(p.draws < 0x7fffffffLL ? p.draws : 0x7fffffffLL),
               4ull * st * (uint64_t)N * (uint64_t)lay.rw < (1ull << 24)};
   InLinks<D> it;
   if constexpr (unrolled(D)) {
@@ -705,7 +707,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
         PW(pi) = (PW(pi) & ~(0xffu << sh)) | ((uint32_t)indeg << sh);
 #pragma unroll
         for (int32_t j = 0; j < D; ++j)
-          if (j < outdeg) push<STAGED>(x, ln, j, kMarkerBit | (uint32_t)op.b, (int64_t)ln.draw + j);
+          if (j < outdeg) push<STAGED>(x, ln, j, kMarkerBit | (uint32_t)op.b, ln.draw + j);
       }
       if (ln.alive) ln.draw += op.c;
       n_started++;
