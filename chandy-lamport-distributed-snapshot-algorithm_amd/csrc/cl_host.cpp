@@ -251,6 +251,9 @@ struct cl_sim {
   // Fold finished launch timings into the accumulator so the event pool stays bounded.
   int fold_events() {
     HIP_TRY(hipStreamSynchronize(stream));
+    // (a pipelined replay's start event is recorded on stream2, which `stream` may not have
+    // joined yet: cl_rerun folds every 256 launches without a join)
+    if (stream2) HIP_TRY(hipStreamSynchronize(stream2));
     for (size_t i = 0; i < ev_used; ++i) {
       float f = 0.f;
       HIP_TRY(hipEventElapsedTime(&f, ev_pool[i].first, ev_pool[i].second));
