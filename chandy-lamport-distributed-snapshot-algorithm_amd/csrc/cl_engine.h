@@ -242,6 +242,7 @@ struct ExecParams {
   uint32_t slot_base;  // first slot of this launch's grid
   int64_t split_slot;
   uint8_t* spill_flag;  // [n_inst] or nullptr
+  int32_t* iters;       // probe runs: [n_inst] tick-loop iterations per instance (the replay order's key), or nullptr
   // slot -> instance for a replay (nullptr: slot i runs instance i).  cl_host orders a
   // replay's instances by their final tick so the segments of a wave finish together
   const int32_t* inst_map;

@@ -61,6 +61,9 @@ constexpr int64_t kMapMinInstances = 4096;
 #ifndef CLSNAP_MAP_PCT
 #define CLSNAP_MAP_PCT 92  // length-ordered slot map when it keeps at most this % of the wave-ticks (A/B knob)
 #endif
+#ifndef CLSNAP_PLAN_KEY
+#define CLSNAP_PLAN_KEY 1  // replay order key: 1 the probe's tick-loop iterations, 0 its final ticks (A/B knob)
+#endif
 #ifndef CLSNAP_LPT
 #define CLSNAP_LPT 1  // slot map order: 1 longest instances first, 0 shortest first (A/B knob)
 #endif
@@ -297,6 +300,7 @@ struct cl_sim {
   // bounds 3-4) and the rest the spill-capable one, concurrently on stream2.  Results are per
   // instance and identical on either kernel.
   DevBuf<uint8_t> d_spill_inst;  // [n_inst] probe: 1 where a push spilled to HBM
+  DevBuf<int32_t> d_iters;       // [n_inst] probe: tick-loop iterations (idle ticks folded)
   int64_t plan_ops = -1;         // program length the plan holds for (-1: none)
   int64_t plan_tried = -1;       // program length a probe last ran for
   bool probe = false;            // the last launch was a probe (plan built at the next sync)
@@ -354,7 +358,7 @@ struct cl_sim {
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
-      d_ovh.release(); d_spill_inst.release(); d_map.release(); d_hist.release(); d_sums.release();
+      d_ovh.release(); d_spill_inst.release(); d_iters.release(); d_map.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       d_pk_tok.release(); d_pk_done.release(); d_pk_msg.release(); d_pk_cnt.release(); d_pk_bsum.release();
       d_pk_off.release(); d_rec2.release();
@@ -568,6 +572,7 @@ struct cl_sim {
     if ((rc = d_ovf.ensure(ov))) return rc;
     if ((rc = d_ovh.ensure(lay.ocap_log2 >= 0 ? (size_t)std::max(C, 1) * stride : 1))) return rc;
     if (lay.ocap_log2 >= 0 && (rc = d_spill_inst.ensure((size_t)n_inst))) return rc;
+    if ((rc = d_iters.ensure((size_t)n_inst))) return rc;
     plan_ops = plan_tried = -1;
     need_fresh = true;
     return CL_OK;
@@ -706,6 +711,7 @@ struct cl_sim {
       HIP_TRY(hipMemsetAsync(d_spill_inst.p, 0, (size_t)n_inst, stream));
       p.spill_flag = d_spill_inst.p;
     }
+    if (probe) p.iters = d_iters.p;
     if (p.split_slot > 0 && !stream2) {
       HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
@@ -778,9 +784,14 @@ struct cl_sim {
     plan_tried = probe_ops;
     plan_map = plan_nospill = false;
     plan_split = plan_spilled = 0;
+    // the length of an instance's replay: its tick-loop iterations (the final tick counts the
+    // idle ticks the kernel folds; CLSNAP_PLAN_KEY 0 sorts by it anyway, an A/B knob)
     std::vector<int32_t> t((size_t)n_inst);
-    HIP_TRY(hipMemcpy2D(t.data(), sizeof(int32_t), d_regs.p + R_TIME, R_NUM * sizeof(int32_t), sizeof(int32_t), t.size(),
-                        hipMemcpyDeviceToHost));
+    if (CLSNAP_PLAN_KEY && d_iters.p)
+      HIP_TRY(hipMemcpy(t.data(), d_iters.p, t.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    else
+      HIP_TRY(hipMemcpy2D(t.data(), sizeof(int32_t), d_regs.p + R_TIME, R_NUM * sizeof(int32_t), sizeof(int32_t),
+                          t.size(), hipMemcpyDeviceToHost));
     std::vector<uint8_t> sp((size_t)n_inst, 0);
     if (probe_flags) HIP_TRY(hipMemcpy(sp.data(), d_spill_inst.p, sp.size(), hipMemcpyDeviceToHost));
     std::vector<int32_t> clean, spilled, ident((size_t)n_inst);

@@ -342,15 +342,44 @@ __device__ __forceinline__ void refill(const Ctx& x, int32_t ko, uint32_t slot) 
   *hp = (h + 1) & om;
 }
 
+// Minimum of v over this lane's instance segment (lanes seg_base .. seg_base + N - 1).
+__device__ __forceinline__ uint32_t seg_min(const Ctx& x, uint32_t v) {
+  const int32_t N = x.p.n_nodes;
+  if (N <= 16 && (N & (N - 1)) == 0) {  // aligned power-of-two segments: DPP butterflies
+    if (N >= 2) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+    if (N >= 4) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+    if (N >= 8) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+    if (N >= 16) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false)); // row_mirror
+    return v;
+  }
+  // any N: suffix minimum inside the segment, then the segment head's value
+  const int32_t last = x.seg_base + N - 1;
+  for (int32_t d = 1; d < N; d <<= 1) v = min(v, (uint32_t)__shfl((int)v, min(x.lane + d, last)));
+  return (uint32_t)__shfl((int)v, x.seg_base);
+}
+
+// Idle-tick folding (A/B knob): a tick in which no head of the instance is due delivers
+// nothing -- every sender peeks each non-empty out-link once (sim.go:81-84) and time advances
+// -- so a run of them is folded into the iteration of the next tick that delivers.
+#ifndef CLSNAP_SKIP
+#define CLSNAP_SKIP 0
+#endif
+
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
 // Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
-// it[] holds this node's in-link words.
+// it[] holds this node's in-link words.  `lim` (>= 1 when act): the ticks the caller may
+// still run.  Returns the reference ticks this call advanced the instance by (0 when !act):
+// idle ticks folded in front of the delivering one, or lim when all of them are idle.
 template <int D, bool STAGED, bool TRACE>
-__device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act) {
+__device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act, int32_t lim) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
   const unsigned long long pt0 = PROF_T();
   ln.time += act ? 1 : 0;
+  int32_t adv = act ? 1 : 0;
+  // earliest head receiveTime over the lane's non-empty out-links not popped (idle folding)
+  uint32_t mrt = 0x7fffffffu;
+  const uint32_t peek0 = ln.peek;
   // ---- A: pick ------------------------------------------------------------
   uint32_t pick = 0, empty_scanned = 0;
   if constexpr (unrolled(D) && CLSNAP_A_PRED) {
@@ -367,7 +396,9 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       empty_scanned |= (look && cnt == 0) ? (1u << ko) : 0u;
       const bool nonempty = look && cnt != 0;
       ln.peek += nonempty ? 1u : 0u;
-      const bool due = nonempty && (int32_t)((e >> 16) & 0x7fffu) <= ln.time;
+      const uint32_t rt = (e >> 16) & 0x7fffu;
+      const bool due = nonempty && (int32_t)rt <= ln.time;
+      if constexpr (CLSNAP_SKIP) mrt = (nonempty && !due) ? min(mrt, rt) : mrt;
       if (__builtin_expect(due && cnt > cap, 0)) refill(x, ko, slot);
       const uint32_t popped = ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
       CHW(ko) = (uint16_t)(due ? popped : chw);
@@ -390,7 +421,10 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       const uint32_t head = chw & (cap - 1);
       const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
       const uint32_t e = PW(slot);
-      if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) continue;
+      if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) {
+        if constexpr (CLSNAP_SKIP) mrt = min(mrt, (e >> 16) & 0x7fffu);
+        continue;
+      }
       if (__builtin_expect(cnt > cap, 0)) refill(x, ko, slot);
       CHW(ko) = (uint16_t)(((cnt - 1) << 8) + ((head + 1) & (cap - 1)));
       pick = (e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16);
@@ -400,6 +434,23 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
   XW(lay.x_pick + x.lane) = pick;
   // Queue.Pop (sim.go:85), counted at the sender: at most one per tick, so 16 bits each
   ln.pops += (pick & kPickValid) ? ((pick & kMarkerBit) ? 0x10000u : 1u) : 0u;
+  if constexpr (CLSNAP_SKIP) {
+    // An instance none of whose senders popped is idle until its earliest head comes due:
+    // the ticks before it only peek every non-empty out-link once more, so they are folded
+    // into this iteration (up to the lim - 1 ticks the caller still allows after this one).
+    const int32_t N = x.p.n_nodes;
+    const uint64_t segm = N == 64 ? ~0ull : (((1ull << N) - 1) << x.seg_base);
+    const bool idle = act && (__ballot((pick & kPickValid) != 0) & segm) == 0;
+    if (__ballot(idle)) {
+      const int32_t smin = (int32_t)seg_min(x, mrt);
+      if (idle) {
+        const int32_t more = min(smin - ln.time, lim) - 1;  // idle ticks after this one
+        ln.peek += (uint32_t)more * (ln.peek - peek0);
+        ln.time += more;
+        adv += more;
+      }
+    }
+  }
   wave_sync();
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
@@ -477,6 +528,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
 #if CLSNAP_PROF
   ln.prof[7] += 1;
 #endif
+  return adv;
 }
 
 // SendTokens (node.go:112-131) of one send event: balance check, link lookup, push -- all
@@ -678,6 +730,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   wave_sync();
   ln.alive = valid && ln.status == ST_OK;
   int32_t n_started = p.n_started_before;
+  uint32_t nit = 0;  // tick-loop iterations this instance was active in (probe runs report them)
 #if CLSNAP_PROF
   PROF_ADD(ln, 5, pro0);
 #endif
@@ -717,9 +770,10 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
       // TICK: op.a ticks.  DRAIN: tick until every started snapshot completed (at most
       // op.a ticks, else HANG), then op.b more (test_common.go:123-137).  Per instance.
       const bool drain = op.kind == OP_DRAIN;
-      int32_t rem = drain ? op.b : op.a;
+      // (rem: ticks left to run; dt: waiting ticks run, per lane -- folded idle ticks count)
+      int32_t rem = drain ? op.b : op.a, dt = 0;
       bool waiting = drain;
-      for (int32_t dt = 0;; ++dt) {
+      for (;;) {
         if (waiting && (!ln.alive || (int32_t)XW(lay.x_ndone + seg) >= n_started)) waiting = false;
         if (waiting && dt >= op.a) {
           ln.status = ST_HANG;
@@ -728,8 +782,10 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
         }
         const bool act = ln.alive && (waiting || rem > 0);
         if (!__ballot(act)) break;
-        tick<D, STAGED, TRACE>(x, ln, it, act);
-        rem -= (act && !waiting) ? 1 : 0;
+        nit += act ? 1u : 0u;
+        const int32_t adv = tick<D, STAGED, TRACE>(x, ln, it, act, waiting ? op.a - dt : rem);
+        if (waiting) dt += adv;
+        else rem -= adv;
       }
 #if CLSNAP_PROF
       PROF_ADD(ln, 4, ot0);
@@ -792,6 +848,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
     r[R_POP_MK] = (int32_t)acc[2];
     r[R_PUSH] = (int32_t)acc[3];
     r[R_INFLIGHT_TOK] = (int32_t)acc[4];
+    if (p.iters) p.iters[ii] = (int32_t)nit;
   }
   if (!p.save_state) return;
   uint32_t* S = p.state + ii;
