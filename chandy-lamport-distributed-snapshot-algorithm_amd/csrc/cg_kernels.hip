@@ -242,8 +242,10 @@ __device__ inline int expand_range(const GParams& p, int32_t t, int32_t s0, int3
     uint32_t b = p.tokcnt[k];
     bool closed = k == karr;  // the arriving channel does not record (node.go:66-69)
     const int32_t src = p.in_src[k];
-    if (src > s0 && p.pick[src] == ((t << 6) | (int32_t)p.in_oj[k])) {  // a later delivery this tick
-      const uint32_t pay = p.ppay[src];
+    // (pick and payload loaded together: one dependent round trip after in_src, not two)
+    const int32_t pk = p.pick[src];
+    const uint32_t pay = p.ppay[src];
+    if (src > s0 && pk == ((t << 6) | (int32_t)p.in_oj[k])) {  // a later delivery this tick
       if (!(pay & kGMarker)) {
         b -= 1;  // delivered after the creating marker: recorded
         tsum += (int)pay;
@@ -499,7 +501,10 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
       if (p.trace)  // SendToNeighbors' SentMsgRecords (node.go:100)
         for (int32_t j = p.out_off[v]; j < p.out_off[v + 1]; ++j)
           gtrace(p, t, kTrTick, (uint32_t)s0, 1u + (uint32_t)(j - p.out_off[v]), TK_SENT_MARKER, v, p.route[j].x, sid);
+      // (both returning atomics issued before either result is used: one round trip)
+      const int add = kBig + (hi - lo) - 1;
       const int slot = atomicAdd(&p.crn[v], 1);
+      const int cold = atomicAdd(&p.cnt[sv], add);
       p.cre[lo + slot] = ((uint64_t)(uint32_t)s0 << 32) | (uint32_t)sid;
       bx = BigX{lo, hi, s0, sid, k, v, {0, 0}};
       if (hi - lo <= kSmallIndeg) {
@@ -508,8 +513,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
         p.stok[sv] = p.tokens[v];  // k_push's expansion subtracts the later same-tick tokens
         bslot = atomicAdd(&s_nb, 1);
       }
-      const int add = kBig + (hi - lo) - 1;
-      done = atomicAdd(&p.cnt[sv], add) + add == kBig;
+      done = cold + add == kBig;
     } else {
       // later marker: stop recording the channel (node.go:158-160)
       if ((key >> 32) != (uint64_t)t) {  // created in an earlier tick: cursors exist
@@ -690,9 +694,8 @@ constexpr int kRegOd = 8;
 template <int R>
 __device__ inline void push_node_reg(const GParams& p, const Bases& bs, int32_t t, int32_t v, int32_t ob, int32_t od,
                                      int ncre, bool send, int32_t tok, int32_t tj, unsigned long long sd,
-                                     unsigned long long (&c)[2]) {
+                                     int32_t lo, unsigned long long (&c)[2]) {
   p.crn[v] = 0;
-  const int32_t lo = p.in_off[v];
   uint32_t srt = 0;
   if (send) {
     // SendTokens(v, out-link tj, 1): node.go:112-131
@@ -743,15 +746,54 @@ __device__ inline void push_node_reg(const GParams& p, const Bases& bs, int32_t 
 // one thread per node): lane jl owns out-channels jl, jl + L, ...; each channel gets the
 // node's broadcasts in creating-sender order, then the traffic send (queue.go:18-20), so
 // per-channel FIFO order is the same as one thread pushing them all.
+constexpr int kRegCre = 4;  // creations per node and tick held in registers by push_node_lanes
 template <int L>
 __device__ inline void push_node_lanes(const GParams& p, const Bases& bs, int32_t t, int32_t v, int32_t ob, int32_t od,
                                        int ncre, bool send, int32_t tok, int32_t tj, unsigned long long sd, int32_t jl,
-                                       unsigned long long (&c)[2]) {
+                                       int32_t lo, unsigned long long (&c)[2]) {
   if (jl == 0) {
     p.crn[v] = 0;
     if (send) p.tokens[v] = tok - 1;  // SendTokens(v, out-link tj, 1): node.go:112-131
   }
-  const int32_t lo = p.in_off[v];
+  if (ncre <= kRegCre) {
+    // the node's creations sorted once into creating-sender order (keys s0 << 32 | sid are
+    // distinct: one delivery per sender and tick) with their draw bases loaded together --
+    // one cre -> ltrig round trip per node instead of one per channel
+    uint64_t cr[kRegCre];
+#pragma unroll
+    for (int i = 0; i < kRegCre; ++i) cr[i] = i < ncre ? p.cre[lo + i] : ~0ull;
+    const int pk = p.pick[v];
+    auto cswap = [](uint64_t& a, uint64_t& b) {
+      const uint64_t x = a < b ? a : b, y = a < b ? b : a;
+      a = x;
+      b = y;
+    };
+    cswap(cr[0], cr[1]);
+    cswap(cr[2], cr[3]);
+    cswap(cr[0], cr[2]);
+    cswap(cr[1], cr[3]);
+    cswap(cr[1], cr[2]);
+    unsigned long long db[kRegCre];
+#pragma unroll
+    for (int i = 0; i < kRegCre; ++i) db[i] = i < ncre ? bdraw(p, bs, (int32_t)(cr[i] >> 32)) : 0ull;
+    // v's own scan peeks the queues the first broadcast made non-empty when its sender
+    // delivered before v's turn (sim.go:82-84)
+    const bool early = (int32_t)(cr[0] >> 32) < v;
+    const int pj = (pk >> 6) == t ? (pk & 63) : 64;
+    for (int32_t j = jl; j < od; j += L) {
+      uint64_t q = p.hq[ob + j];
+      if (early && j < pj && (uint32_t)q == kEmpty) ++c[1];
+#pragma unroll
+      for (int r = 0; r < kRegCre; ++r)
+        if (r < ncre) push_q(p, ob + j, q, kGMarker | (uint32_t)cr[r], receive_time(p, db[r] + (unsigned long long)j, t), c[0]);
+      if (send && j == tj) {
+        push_q(p, ob + j, q, 1u, receive_time(p, sd, t), c[0]);
+        gtrace(p, t, kTrSend, (uint32_t)v, 0u, TK_SENT_TOKEN, v, p.route[ob + j].x, 1);  // node.go:118
+      }
+      p.hq[ob + j] = q;
+    }
+    return;
+  }
   for (int32_t j = jl; j < od; j += L) {
     uint64_t q = p.hq[ob + j];
     uint64_t prev = 0;
@@ -791,7 +833,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
   const int32_t step = sarg >= 0 ? sarg : t;  // the traffic of step t follows tick t
   const int64_t gid = ((int64_t)p.blk_lo * kGThreads * L) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int v = (int)(gid / L), jl = (int)(gid % L);
-  int32_t ob = 0, od = 0, ncre = 0, tok = 0, tj = -1;
+  int32_t ob = 0, od = 0, ncre = 0, tok = 0, tj = -1, ilo = 0;
   bool send = false;
   uint64_t q0 = 0;
   unsigned long long sd = 0;
@@ -799,6 +841,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
     ob = p.out_off[v];
     od = p.out_off[v + 1] - ob;
     ncre = p.crn[v];
+    ilo = p.in_off[v];  // (the creation slots' base: off the creation path's load chain)
     tok = p.tokens[v];
     // the traffic decision and what its push reads: the draw index (k_scan's bases, the
     // block tally) and, for a node without broadcasts, the channel's head word
@@ -859,8 +902,8 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
   unsigned long long c[2] = {0, 0};  // push, peek
   if (v < p.part_hi) {
     if (ncre) {
-      if constexpr (L == 1) push_node_reg<kRegOd>(p, bs, t, v, ob, od, ncre, send, tok, tj, sd, c);
-      else push_node_lanes<L>(p, bs, t, v, ob, od, ncre, send, tok, tj, sd, jl, c);
+      if constexpr (L == 1) push_node_reg<kRegOd>(p, bs, t, v, ob, od, ncre, send, tok, tj, sd, ilo, c);
+      else push_node_lanes<L>(p, bs, t, v, ob, od, ncre, send, tok, tj, sd, jl, ilo, c);
     } else if (send && jl == 0) {
       // SendTokens(v, out-link j, 1): node.go:112-131 (one channel: no batching)
       p.tokens[v] = tok - 1;
