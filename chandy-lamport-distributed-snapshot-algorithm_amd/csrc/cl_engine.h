@@ -209,6 +209,15 @@ struct ColumnC {
                            w_pend = w_trig + (D + 1) / 2;
 };
 
+// Idle-tick folding in the exec kernel (A/B knob, off: DESIGN.md §9): a tick in which no
+// head of an instance is due delivers nothing -- every sender peeks each non-empty out-link
+// once (sim.go:81-84) and time advances -- so a run of them can be folded into one iteration.
+// With it the probe reports tick-loop iterations (ExecParams::iters), the replay order's key.
+// 2: only ticks of an instance whose queues are all empty are folded (the rest of a drain).
+#ifndef CLSNAP_SKIP
+#define CLSNAP_SKIP 0
+#endif
+
 // Kernel parameters (passed by value).
 struct ExecParams {
   int32_t op_begin, op_end;

@@ -711,7 +711,7 @@ struct cl_sim {
       HIP_TRY(hipMemsetAsync(d_spill_inst.p, 0, (size_t)n_inst, stream));
       p.spill_flag = d_spill_inst.p;
     }
-    if (probe) p.iters = d_iters.p;
+    if (probe && CLSNAP_SKIP) p.iters = d_iters.p;
     if (p.split_slot > 0 && !stream2) {
       HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
@@ -787,7 +787,7 @@ struct cl_sim {
     // the length of an instance's replay: its tick-loop iterations (the final tick counts the
     // idle ticks the kernel folds; CLSNAP_PLAN_KEY 0 sorts by it anyway, an A/B knob)
     std::vector<int32_t> t((size_t)n_inst);
-    if (CLSNAP_PLAN_KEY && d_iters.p)
+    if (CLSNAP_SKIP && CLSNAP_PLAN_KEY && d_iters.p)
       HIP_TRY(hipMemcpy(t.data(), d_iters.p, t.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
     else
       HIP_TRY(hipMemcpy2D(t.data(), sizeof(int32_t), d_regs.p + R_TIME, R_NUM * sizeof(int32_t), sizeof(int32_t),

@@ -124,6 +124,7 @@ struct Lane {
   int32_t time, draw, status;
   uint32_t peek, push;
   uint32_t pops;  // packets this node delivered as a sender: tokens (lo16) | markers (hi16); <= 1 per tick
+  uint32_t cur[2];  // (cursors in registers, unrolled D <= 4) in-link k's recording cursor: u16 k & 1 of word k >> 1
   bool alive;    // instance still running (uniform within the segment)
   int32_t flag;  // lane-local engine failure raised during an op/tick
 #if CLSNAP_PROF
@@ -156,6 +157,18 @@ struct Lane {
 constexpr bool unrolled(int D) { return D <= CLSNAP_UNROLL_MAX; }
 template <int D>
 using InLinks = uint32_t[unrolled(D) ? D : 1];
+// In-link recording cursors (delivered-token counts) of the unrolled kernels live in two
+// packed registers instead of the link words' hi16 halves (A/B knob): phase B's per-in-link
+// LDS read + write becomes one add.  The LDS halves are refreshed only for the state image.
+#ifndef CLSNAP_CURREG
+#define CLSNAP_CURREG 0
+#endif
+// Phase A stores only the popped link's head word (one store at a runtime offset) instead of
+// one predicated store per out-link (A/B knob).
+#ifndef CLSNAP_POPW
+#define CLSNAP_POPW 0
+#endif
+constexpr bool cur_reg(int D) { return CLSNAP_CURREG && D <= 4 && unrolled(D); }
 
 #define PW(k) (x.P[(uint32_t)(k) << 6])
 #define XW(k) (x.X[(uint32_t)(k)])
@@ -166,6 +179,24 @@ using InLinks = uint32_t[unrolled(D) ? D : 1];
 #define CUR(ki) PH(lay.w_lnk + (ki), 1)
 // trigger entry k (16 bit: sender rank | snapshot id << 8)
 #define TRIG(k) PH(lay.w_trig + ((uint32_t)(k) >> 1), (k) & 1)
+
+// In-link k's recording cursor (k < D; a compile-time index in the unrolled kernels).
+template <int D>
+__device__ __forceinline__ uint32_t cur_get(const Ctx& x, const Lane& ln, int32_t k) {
+  if constexpr (cur_reg(D)) return (ln.cur[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+  const Layout& lay = x.lay;
+  return CUR(k);
+}
+template <int D>
+__device__ __forceinline__ void cur_add(const Ctx& x, Lane& ln, int32_t k, bool tok) {
+  if constexpr (cur_reg(D)) {
+    ln.cur[k >> 1] += tok ? (1u << ((k & 1) * 16)) : 0u;  // (<= 65,535 tokens per channel: no carry)
+  } else {
+    const Layout& lay = x.lay;
+    const uint32_t c = CUR(k);
+    CUR(k) = (uint16_t)(c + (tok ? 1u : 0u));
+  }
+}
 
 // LDS atomic add (ds_add_rtn_u32); the wave's lanes are the only users of these words.
 __device__ __forceinline__ uint32_t lds_add(lds_u32* a, uint32_t v) {
@@ -241,7 +272,7 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
     r[0] = (uint32_t)ln.tokens;
 #pragma unroll
     for (int32_t kj = 0; kj < RW - 1; ++kj) {
-      const uint32_t cur = (kj < D && kj < x.indeg) ? (uint32_t)CUR(kj) : 0u;
+      const uint32_t cur = (kj < D && kj < x.indeg) ? cur_get<D>(x, ln, kj) : 0u;
       r[1 + kj] = kj == arrive ? (cur | (cur << 16)) : cur;
     }
     (void)it;
@@ -320,7 +351,7 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
     // hi16 of the cursor word: the channel's end
     st_snap(reinterpret_cast<uint16_t*>(x.p.snap_nod),
           plane_off(x, (uint32_t)sid, x.nod_plane) + nod_lane(x) + 4u * (1 + (uint32_t)ki) + 2u,
-          (uint16_t)CUR(ki));
+          (uint16_t)cur_get<D>(x, ln, ki));
     pend = ((pw >> sh) & 0xffu) - 1;
   }
   PW(pi) = (pw & ~(0xffu << sh)) | (pend << sh);
@@ -358,13 +389,6 @@ __device__ __forceinline__ uint32_t seg_min(const Ctx& x, uint32_t v) {
   return (uint32_t)__shfl((int)v, x.seg_base);
 }
 
-// Idle-tick folding (A/B knob): a tick in which no head of the instance is due delivers
-// nothing -- every sender peeks each non-empty out-link once (sim.go:81-84) and time advances
-// -- so a run of them is folded into the iteration of the next tick that delivers.
-#ifndef CLSNAP_SKIP
-#define CLSNAP_SKIP 0
-#endif
-
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
 // Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
 // it[] holds this node's in-link words.  `lim` (>= 1 when act): the ticks the caller may
@@ -380,8 +404,10 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
   // earliest head receiveTime over the lane's non-empty out-links not popped (idle folding)
   uint32_t mrt = 0x7fffffffu;
   const uint32_t peek0 = ln.peek;
+  bool anyq = false;  // (CLSNAP_SKIP 2) a non-empty out-link at tick start
   // ---- A: pick ------------------------------------------------------------
   uint32_t pick = 0, empty_scanned = 0;
+  uint32_t pw_val = 0;  // (CLSNAP_POPW) the popped link's new head word
   if constexpr (unrolled(D) && CLSNAP_A_PRED) {
     bool scanning = act;
 #pragma unroll
@@ -398,13 +424,18 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
       ln.peek += nonempty ? 1u : 0u;
       const uint32_t rt = (e >> 16) & 0x7fffu;
       const bool due = nonempty && (int32_t)rt <= ln.time;
-      if constexpr (CLSNAP_SKIP) mrt = (nonempty && !due) ? min(mrt, rt) : mrt;
+      if constexpr (CLSNAP_SKIP == 1) mrt = (nonempty && !due) ? min(mrt, rt) : mrt;
+      if constexpr (CLSNAP_SKIP == 2) anyq = anyq || nonempty;
       if (__builtin_expect(due && cnt > cap, 0)) refill(x, ko, slot);
       const uint32_t popped = ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
-      CHW(ko) = (uint16_t)(due ? popped : chw);
+      if constexpr (CLSNAP_POPW) pw_val = due ? popped : pw_val;
+      else CHW(ko) = (uint16_t)(due ? popped : chw);
       pick = due ? ((e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16)) : pick;
       scanning = scanning && !due;
     }
+    // (CLSNAP_POPW) one head-word store, the popped link's, at its runtime column offset
+    if constexpr (CLSNAP_POPW)
+      if (pick & kPickValid) PH(lay.w_lnk + ((pick >> 16) & 0x7fu), 0) = (uint16_t)pw_val;
   } else if (act) {
     bool done = false;
 #pragma unroll
@@ -421,8 +452,9 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
       const uint32_t head = chw & (cap - 1);
       const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
       const uint32_t e = PW(slot);
+      if constexpr (CLSNAP_SKIP == 2) anyq = true;
       if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) {
-        if constexpr (CLSNAP_SKIP) mrt = min(mrt, (e >> 16) & 0x7fffu);
+        if constexpr (CLSNAP_SKIP == 1) mrt = min(mrt, (e >> 16) & 0x7fffu);
         continue;
       }
       if (__builtin_expect(cnt > cap, 0)) refill(x, ko, slot);
@@ -434,7 +466,16 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
   XW(lay.x_pick + x.lane) = pick;
   // Queue.Pop (sim.go:85), counted at the sender: at most one per tick, so 16 bits each
   ln.pops += (pick & kPickValid) ? ((pick & kMarkerBit) ? 0x10000u : 1u) : 0u;
-  if constexpr (CLSNAP_SKIP) {
+  if constexpr (CLSNAP_SKIP == 2) {
+    // An instance whose queues are all empty at tick start delivers nothing in any tick
+    // the caller still allows (no events run inside the loop): they are all folded here.
+    const bool empty = act && seg_min(x, anyq ? 0u : 1u) != 0;
+    if (__ballot(empty) && empty) {
+      ln.time += lim - 1;
+      adv = lim;
+    }
+  }
+  if constexpr (CLSNAP_SKIP == 1) {
     // An instance none of whose senders popped is idle until its earliest head comes due:
     // the ticks before it only peek every non-empty out-link once more, so they are folded
     // into this iteration (up to the lim - 1 ticks the caller still allows after this one).
@@ -469,8 +510,7 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
         if (m) temit<TRACE>(x, mk ? TK_RECV_MARKER : TK_RECV_TOKEN, src, ln.time, src << 8, (int32_t)pay, ln.tokens);
       // HandleToken: tokens += data; the channel's recording cursor advances
       ln.tokens += tok ? (int32_t)pay : 0;
-      const uint32_t cur = CUR(ki);
-      CUR(ki) = (uint16_t)(cur + (tok ? 1u : 0u));
+      cur_add<D>(x, ln, ki, tok);
       if (mk) handle_marker<D, TRACE>(x, ln, it, ki, w, src, (int32_t)pay, ntrig);
     }
   } else if (act) {
@@ -486,7 +526,7 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
                    ln.tokens);
       if (!(pk & kMarkerBit)) {  // HandleToken: tokens += data; the recording cursor advances
         ln.tokens += (int32_t)pay;
-        CUR(ki) = (uint16_t)(CUR(ki) + 1u);
+        cur_add<D>(x, ln, ki, true);
         continue;
       }
       handle_marker<D, TRACE>(x, ln, it, ki, w, src, (int32_t)pay, ntrig);
@@ -727,10 +767,16 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   }
   if constexpr (!unrolled(D))
     for (int32_t k = 0; k < indeg; ++k) PW(lay.w_int + k) = nb[3 + k];
+  ln.cur[0] = ln.cur[1] = 0;
+  if constexpr (cur_reg(D)) {
+#pragma unroll
+    for (int32_t k = 0; k < D; ++k)
+      if (k < indeg) ln.cur[k >> 1] |= (uint32_t)CUR(k) << ((k & 1) * 16);
+  }
   wave_sync();
   ln.alive = valid && ln.status == ST_OK;
   int32_t n_started = p.n_started_before;
-  uint32_t nit = 0;  // tick-loop iterations this instance was active in (probe runs report them)
+  uint32_t nit = 0;  // (idle folding) tick-loop iterations this instance was active in, for the probe
 #if CLSNAP_PROF
   PROF_ADD(ln, 5, pro0);
 #endif
@@ -771,21 +817,22 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
       // op.a ticks, else HANG), then op.b more (test_common.go:123-137).  Per instance.
       const bool drain = op.kind == OP_DRAIN;
       // (rem: ticks left to run; dt: waiting ticks run, per lane -- folded idle ticks count)
+      // (without folding every waiting lane runs one tick per iteration: the uniform loop count)
       int32_t rem = drain ? op.b : op.a, dt = 0;
       bool waiting = drain;
-      for (;;) {
+      for (int32_t iter = 0;; ++iter) {
         if (waiting && (!ln.alive || (int32_t)XW(lay.x_ndone + seg) >= n_started)) waiting = false;
-        if (waiting && dt >= op.a) {
+        if (waiting && (CLSNAP_SKIP ? dt : iter) >= op.a) {
           ln.status = ST_HANG;
           ln.alive = false;
           waiting = false;
         }
         const bool act = ln.alive && (waiting || rem > 0);
         if (!__ballot(act)) break;
-        nit += act ? 1u : 0u;
-        const int32_t adv = tick<D, STAGED, TRACE>(x, ln, it, act, waiting ? op.a - dt : rem);
-        if (waiting) dt += adv;
-        else rem -= adv;
+        if constexpr (CLSNAP_SKIP) nit += act ? 1u : 0u;
+        const int32_t adv = tick<D, STAGED, TRACE>(x, ln, it, act, waiting ? op.a - (CLSNAP_SKIP ? dt : iter) : rem);
+        if (CLSNAP_SKIP && waiting) dt += adv;
+        else if (!waiting) rem -= adv;
       }
 #if CLSNAP_PROF
       PROF_ADD(ln, 4, ot0);
@@ -848,9 +895,14 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
     r[R_POP_MK] = (int32_t)acc[2];
     r[R_PUSH] = (int32_t)acc[3];
     r[R_INFLIGHT_TOK] = (int32_t)acc[4];
-    if (p.iters) p.iters[ii] = (int32_t)nit;
+    if (CLSNAP_SKIP && p.iters) p.iters[ii] = (int32_t)nit;
   }
   if (!p.save_state) return;
+  if constexpr (cur_reg(D)) {  // the link words' cursor halves, for the state image
+#pragma unroll
+    for (int32_t k = 0; k < D; ++k)
+      if (k < indeg) CUR(k) = (uint16_t)cur_get<D>(x, ln, k);
+  }
   uint32_t* S = p.state + ii;
   const uint32_t b = (uint32_t)v * (lay.priv + G_NUM);
   for (int32_t k = 0; k < lay.priv; ++k) S[(b + k) * st] = PW(k);
