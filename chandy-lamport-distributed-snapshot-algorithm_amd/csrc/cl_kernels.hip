@@ -161,7 +161,7 @@ using InLinks = uint32_t[unrolled(D) ? D : 1];
 // packed registers instead of the link words' hi16 halves (A/B knob): phase B's per-in-link
 // LDS read + write becomes one add.  The LDS halves are refreshed only for the state image.
 #ifndef CLSNAP_CURREG
-#define CLSNAP_CURREG 0
+#define CLSNAP_CURREG 1
 #endif
 // Phase A stores only the popped link's head word (one store at a runtime offset) instead of
 // one predicated store per out-link (A/B knob).
