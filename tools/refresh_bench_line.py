@@ -18,8 +18,8 @@ lines = [ln for ln in open(path) if ln.lstrip().startswith("{")]
 d = json.loads(lines[-1])
 prof = bench.profile_entry(cfg, d["config"]["instances_per_gpu"])
 if prof is not None:
-    p, doc = prof
-    c = doc["counters"]
+    p, doc, scale = prof
+    c = {k: (v * scale if k != "SQ_WAVE_CYCLES" and k != "GRBM_GUI_ACTIVE" else v) for k, v in doc["counters"].items()}
     r = d["roofline"]
     kms = r["kernel_ms"]
     r["traffic"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
