@@ -124,6 +124,7 @@ struct Lane {
   int32_t time, draw, status;
   uint32_t peek, push;
   uint32_t pops;  // packets this node delivered as a sender: tokens (lo16) | markers (hi16); <= 1 per tick
+  uint32_t hw[2];   // (head words in registers, unrolled D <= 4) out-link k's head word: u16 k & 1 of word k >> 1
   uint32_t cur[2];  // (cursors in registers, unrolled D <= 4) in-link k's recording cursor: u16 k & 1 of word k >> 1
   bool alive;    // instance still running (uniform within the segment)
   int32_t flag;  // lane-local engine failure raised during an op/tick
@@ -168,6 +169,13 @@ using InLinks = uint32_t[unrolled(D) ? D : 1];
 #ifndef CLSNAP_POPW
 #define CLSNAP_POPW 0
 #endif
+// Out-link head words (8-bit ring head, 8-bit count) of the unrolled kernels in two packed
+// registers instead of the link words' lo16 halves (A/B knob): phase A's and the pushes' LDS
+// reads + writes become register ops; the halves are refreshed for the epilogue.
+#ifndef CLSNAP_HWREG
+#define CLSNAP_HWREG 0
+#endif
+constexpr bool hw_reg(int D) { return CLSNAP_HWREG && D <= 4 && CLSNAP_UNROLL_MAX >= D; }
 constexpr bool cur_reg(int D) { return CLSNAP_CURREG && D <= 4 && unrolled(D); }
 
 #define PW(k) (x.P[(uint32_t)(k) << 6])
@@ -179,6 +187,24 @@ constexpr bool cur_reg(int D) { return CLSNAP_CURREG && D <= 4 && unrolled(D); }
 #define CUR(ki) PH(lay.w_lnk + (ki), 1)
 // trigger entry k (16 bit: sender rank | snapshot id << 8)
 #define TRIG(k) PH(lay.w_trig + ((uint32_t)(k) >> 1), (k) & 1)
+
+// Out-link k's head word (k < D: a compile-time index in the unrolled kernels).
+template <int D>
+__device__ __forceinline__ uint32_t hw_get(const Ctx& x, const Lane& ln, int32_t k) {
+  if constexpr (hw_reg(D)) return (ln.hw[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+  const Layout& lay = x.lay;
+  return CHW(k);
+}
+template <int D>
+__device__ __forceinline__ void hw_set(const Ctx& x, Lane& ln, int32_t k, uint32_t v) {
+  if constexpr (hw_reg(D)) {
+    const uint32_t sh = (k & 1) * 16;
+    ln.hw[k >> 1] = (ln.hw[k >> 1] & ~(0xffffu << sh)) | ((v & 0xffffu) << sh);
+  } else {
+    const Layout& lay = x.lay;
+    CHW(k) = (uint16_t)v;
+  }
+}
 
 // In-link k's recording cursor (k < D; a compile-time index in the unrolled kernels).
 template <int D>
@@ -225,11 +251,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // are staged in LDS.  A compile-time choice: with an HBM delay load anywhere on the path
 // the compiler waits with s_waitcnt vmcnt(0) at the join, and on gfx950 vmcnt also counts
 // the wave's outstanding global STORES (snapshot outputs) -- a full store drain per push.
-template <bool STAGED>
+template <int D, bool STAGED>
 __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int32_t k) {
   const Layout& lay = x.lay;
   if (k >= x.draws) { ln.flag = ST_DELAY_EXHAUSTED; return; }
-  const uint32_t chw = CHW(ko);
+  const uint32_t chw = hw_get<D>(x, ln, ko);
   const uint32_t cnt = chw >> 8;
   if (cnt >= (uint32_t)kMaxQueued) { ln.flag = ST_FIFO_OVERFLOW; return; }
   uint32_t delay;
@@ -252,7 +278,7 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
     x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.stride + x.inst] = e;
     if (x.p.spill_flag) x.p.spill_flag[x.inst] = 1;  // (the replay plan: this instance needs the rings)
   }
-  CHW(ko) = (uint16_t)(chw + kCountOne);
+  hw_set<D>(x, ln, ko, chw + kCountOne);
   ln.push++;
 }
 
@@ -414,7 +440,7 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
     for (int32_t ko = 0; ko < D; ++ko) {
       if (ko >= lay.od) break;  // uniform: the layout holds od out-links per lane
       const bool look = scanning && ko < x.outdeg;
-      const uint32_t chw = CHW(ko);
+      const uint32_t chw = hw_get<D>(x, ln, ko);
       const uint32_t cnt = chw >> 8;
       const uint32_t head = chw & (cap - 1);
       const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
@@ -429,7 +455,7 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
       if (__builtin_expect(due && cnt > cap, 0)) refill(x, ko, slot);
       const uint32_t popped = ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
       if constexpr (CLSNAP_POPW) pw_val = due ? popped : pw_val;
-      else CHW(ko) = (uint16_t)(due ? popped : chw);
+      else hw_set<D>(x, ln, ko, due ? popped : chw);
       pick = due ? ((e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16)) : pick;
       scanning = scanning && !due;
     }
@@ -442,7 +468,7 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
     for (int32_t ko = 0; ko < (unrolled(D) ? D : x.outdeg); ++ko) {
       if (ko >= x.outdeg) break;
       if (done) continue;
-      const uint32_t chw = CHW(ko);
+      const uint32_t chw = hw_get<D>(x, ln, ko);
       const uint32_t cnt = chw >> 8;
       if (!cnt) {
         empty_scanned |= 1u << ko;
@@ -458,7 +484,7 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
         continue;
       }
       if (__builtin_expect(cnt > cap, 0)) refill(x, ko, slot);
-      CHW(ko) = (uint16_t)(((cnt - 1) << 8) + ((head + 1) & (cap - 1)));
+      hw_set<D>(x, ln, ko, ((cnt - 1) << 8) + ((head + 1) & (cap - 1)));
       pick = (e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16);
       done = true;
     }
@@ -552,7 +578,7 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
 #pragma unroll
       for (int32_t j = 0; j < D; ++j) {
         if (j >= x.outdeg) continue;
-        push<STAGED>(x, ln, j, kMarkerBit | sid, k0 + j);
+        push<D, STAGED>(x, ln, j, kMarkerBit | sid, k0 + j);
         // the reference scans this sender's links after the push when the trigger came
         // from a lower rank: a link that was empty at tick start gets peeked once more
         if ((int32_t)src < x.v && ((empty_scanned >> j) & 1u)) {
@@ -586,7 +612,7 @@ __device__ __forceinline__ void send_one(const Ctx& x, Lane& ln, const Op& op, i
     ln.tokens -= op.c;
 #pragma unroll
     for (int32_t j = 0; j < D; ++j)  // static register indices for the out-link
-      if (j == op.b) push<STAGED>(x, ln, j, (uint32_t)op.c, ln.draw);
+      if (j == op.b) push<D, STAGED>(x, ln, j, (uint32_t)op.c, ln.draw);
   }
   if (ln.alive) {
     if (fatal) {
@@ -625,7 +651,14 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
     if (ln.tokens < on || oj < 0 || ln.draw + pos >= x.draws) {
       bad = true;
     } else {  // the checks push() makes
-      const uint32_t cnt = (uint32_t)CHW(oj) >> 8, cap = 1u << lay.cap_log2;
+      uint32_t chw = 0;
+      if constexpr (hw_reg(D)) {
+#pragma unroll
+        for (int32_t j = 0; j < D; ++j) chw = j == oj ? hw_get<D>(x, ln, j) : chw;
+      } else {
+        chw = CHW(oj);
+      }
+      const uint32_t cnt = chw >> 8, cap = 1u << lay.cap_log2;
       bad = cnt >= (uint32_t)kMaxQueued || (cnt >= cap && (lay.ocap_log2 < 0 || cnt - cap >= (1u << lay.ocap_log2)));
     }
   }
@@ -639,7 +672,7 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
     ln.tokens -= on;
 #pragma unroll
     for (int32_t j = 0; j < D; ++j)
-      if (j == oj) push<STAGED>(x, ln, j, (uint32_t)on, ln.draw + pos);
+      if (j == oj) push<D, STAGED>(x, ln, j, (uint32_t)on, ln.draw + pos);
   }
   if (ln.alive) ln.draw += k;
 }
@@ -768,6 +801,12 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   if constexpr (!unrolled(D))
     for (int32_t k = 0; k < indeg; ++k) PW(lay.w_int + k) = nb[3 + k];
   ln.cur[0] = ln.cur[1] = 0;
+  ln.hw[0] = ln.hw[1] = 0;
+  if constexpr (hw_reg(D)) {
+#pragma unroll
+    for (int32_t k = 0; k < D; ++k)
+      if (k < lay.od) ln.hw[k >> 1] |= (uint32_t)CHW(k) << ((k & 1) * 16);
+  }
   if constexpr (cur_reg(D)) {
 #pragma unroll
     for (int32_t k = 0; k < D; ++k)
@@ -806,7 +845,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
         PW(pi) = (PW(pi) & ~(0xffu << sh)) | ((uint32_t)indeg << sh);
 #pragma unroll
         for (int32_t j = 0; j < D; ++j)
-          if (j < outdeg) push<STAGED>(x, ln, j, kMarkerBit | (uint32_t)op.b, ln.draw + j);
+          if (j < outdeg) push<D, STAGED>(x, ln, j, kMarkerBit | (uint32_t)op.b, ln.draw + j);
       }
       if (ln.alive) ln.draw += op.c;
       n_started++;
@@ -844,6 +883,11 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
 #endif
 
   // ---- epilogue: tokens still queued, per-instance sums, outputs, state image ------
+  if constexpr (hw_reg(D)) {  // the link words' head halves
+#pragma unroll
+    for (int32_t k = 0; k < D; ++k)
+      if (k < lay.od) CHW(k) = (uint16_t)hw_get<D>(x, ln, k);
+  }
   int32_t inflight = 0;
   {
     const uint32_t cap = 1u << lay.cap_log2;
