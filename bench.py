@@ -13,7 +13,9 @@ oracle's values for the same instances (tests/golden/bench_sums.json): "parity".
 Multi-GPU: one process per GPU; the fixed 2^20-instance batch is split into disjoint
 instance ranges (rank r: instances [r*I/N, (r+1)*I/N), seeds base + global index), so
 there is no data-path collective ("scaling": "strong"); RCCL all-reduces the batch
-checksums once, after timing.  --config c2 is BASELINE config 2 (10nodes x 65,536);
+checksums once, after timing.  `bench.py --gpus N` run by hand starts the N ranks itself
+(a child torch.distributed.run); under the driver's own torch.distributed.run each rank
+checks that WORLD_SIZE equals --gpus.  --config c2 is BASELINE config 2 (10nodes x 65,536);
 c4/c5 are the large-graph configs (one simulation per GPU, replicas).
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §6 for the byte model behind "roofline".
@@ -82,7 +84,7 @@ PARITY_KEYS = ("instances", "ok", "fatal", "other", "delivered", "snapshot_hash"
 STEP_DEFAULTS = {"c2": (300, 100), "c3": (20, 10)}
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default: per config, STEP_DEFAULTS)")
@@ -102,11 +104,77 @@ def parse_args():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on GPUs; gloo for rehearsals")
     ap.add_argument("--shared-device", action="store_true",
                     help="every rank on cuda:0 (multi-rank rehearsal on a one-GPU box)")
-    args = ap.parse_args()
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test hook: ranks rendezvous over gloo, rank 0 prints the world it saw, no GPU work")
+    args = ap.parse_args(argv)
     steps, warmup = STEP_DEFAULTS.get(args.config, (20, 3))
     args.steps = steps if args.steps is None else args.steps
     args.warmup = warmup if args.warmup is None else args.warmup
     return args
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(args, env, argv):
+    """How this process runs `--gpus N` (one process per GPU).
+
+    Returns None when this process is a rank already (WORLD_SIZE set and equal to
+    --gpus) or the run is single-GPU; else the torch.distributed.run command that starts
+    N ranks of this script with the same arguments.  A WORLD_SIZE that differs from
+    --gpus is an error (SystemExit, non-zero): the line would report a world it was not
+    asked to measure."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}: refusing to measure a "
+                             f"different world than the one asked for")
+        return None
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus}")
+    if args.gpus == 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
+def relaunch(args, argv):
+    """`bench.py --gpus N` started by hand (no WORLD_SIZE): start the N ranks as a child
+    torch.distributed.run before anything here touches the GPU, let rank 0's JSON line
+    through, and return the child's exit code.  None: this process runs the bench."""
+    cmd = launch_plan(args, os.environ, argv)
+    if cmd is None:
+        return None
+    if not args.shared_device and not args.launch_check:
+        import torch   # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but {have} visible GPU(s) "
+                             f"(--shared-device rehearses N ranks on one GPU)")
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(args, rank, world):
+    """--launch-check: the rank launch alone (rendezvous + one gloo all-reduce), no GPU."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")
+    t = torch.tensor([rank, 1], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": int(t[1]),
+                          "rank_sum": int(t[0]), "gpus_arg": args.gpus}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def init_dist(args, world, local_rank):
@@ -137,11 +205,17 @@ def profile_entry(cfg, instances):
     return exact or near
 
 
-def main():
-    args = parse_args()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    rc = relaunch(args, argv)
+    if rc is not None:
+        return rc
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        return launch_check(args, rank, world)
     if args.config in GRAPH_CONFIGS:
         return bench_graph(args, rank, world, local_rank)
     top, events, total, desc = CONFIGS[args.config]
@@ -636,4 +710,4 @@ def cpu_baseline(top, events, n_total, budget_s):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -329,13 +329,23 @@ class ChandyLamportSim:
         """CollectSnapshot of many instances packed on the GPU (cl_collect_snapshot_packed):
         (tokens int32[n, N], complete bool[n], offsets int64[n * C + 1], messages int32).
         `out` = (tokens, complete, offsets, messages) arrays to fill (reused across calls; the
-        message array is grown when too small)."""
+        message array is grown when too small: the returned messages are a view of the array
+        actually filled, so pass that base array back in `out` to reuse it)."""
         hi = self.n_instances if inst_hi is None else inst_hi
         k, n, ch = hi - inst_lo, self.num_nodes, self.num_channels
         if out is None:
             out = (np.zeros((k, n), dtype=np.int32), np.zeros(k, dtype=np.int32),
                    np.zeros(k * ch + 1, dtype=np.int64), np.zeros(max(1024, 4 * k), dtype=np.int32))
         tok, done, off, msg = out
+        # the C side writes k * N tokens, k flags, k * C + 1 offsets: a buffer sized for another
+        # range would be overrun
+        for name, a, shape, dt in (("tokens", tok, (k, n), np.int32), ("complete", done, (k,), np.int32),
+                                   ("offsets", off, (k * ch + 1,), np.int64)):
+            if not isinstance(a, np.ndarray) or a.shape != shape or a.dtype != dt or not a.flags.c_contiguous:
+                raise ValueError(f"collect_snapshot_packed: out {name} must be a C-contiguous {np.dtype(dt)} array "
+                                 f"of shape {shape}")
+        if not isinstance(msg, np.ndarray) or msg.dtype != np.int32 or msg.ndim != 1 or not msg.flags.c_contiguous:
+            raise ValueError("collect_snapshot_packed: out messages must be a C-contiguous 1-d int32 array")
         m = C.c_int64(0)
         rc = self._L.cl_collect_snapshot_packed(self._h, snapshot_id, inst_lo, hi, _p(tok), _p(done), _p(off),
                                                 _p(msg), msg.size, C.byref(m))

@@ -203,7 +203,10 @@ struct cl_graph {
   ~cl_graph() {
     if (!dev_ready) return;
     (void)hipSetDevice(device);
+    // both streams drain before any buffer is freed: the caller's (cl_graph_set_stream) and
+    // the engine's own, which may hold work issued before the switch
     (void)hipStreamSynchronize(stream);
+    if (own_stream != stream) (void)hipStreamSynchronize(own_stream);
     GBuf<int32_t>* i32s[] = {&d_out_off, &d_in_off, &d_in_src, &d_init_tok, &d_tokens,
                              &d_pick,    &d_ltrig,  &d_lsend,    &d_crn,    &d_mcnt,   &d_cnt,      &d_stok,
                              &d_done,    &d_ctick};

@@ -209,15 +209,6 @@ struct ColumnC {
                            w_pend = w_trig + (D + 1) / 2;
 };
 
-// Idle-tick folding in the exec kernel (A/B knob, off: DESIGN.md §9): a tick in which no
-// head of an instance is due delivers nothing -- every sender peeks each non-empty out-link
-// once (sim.go:81-84) and time advances -- so a run of them can be folded into one iteration.
-// With it the probe reports tick-loop iterations (ExecParams::iters), the replay order's key.
-// 2: only ticks of an instance whose queues are all empty are folded (the rest of a drain).
-#ifndef CLSNAP_SKIP
-#define CLSNAP_SKIP 0
-#endif
-
 // Kernel parameters (passed by value).
 struct ExecParams {
   int32_t op_begin, op_end;
@@ -251,7 +242,6 @@ struct ExecParams {
   uint32_t slot_base;  // first slot of this launch's grid
   int64_t split_slot;
   uint8_t* spill_flag;  // [n_inst] or nullptr
-  int32_t* iters;       // probe runs: [n_inst] tick-loop iterations per instance (the replay order's key), or nullptr
   // slot -> instance for a replay (nullptr: slot i runs instance i).  cl_host orders a
   // replay's instances by their final tick so the segments of a wave finish together
   const int32_t* inst_map;
@@ -297,6 +287,11 @@ struct ExecLaunch {
   // stream (new work there since the last fork), join = the engine stream waits for stream2
   // before the stop event (else the join is deferred to the next call that is not a rerun)
   int32_t fork, join;
+  // split replays: the spill-capable dispatch records this stop event of its own (it may end
+  // after the main stream's stop event when the replays are not joined); *stop2_used is set
+  // to 1 when it was recorded, and the launch time is the later of the two stops
+  void* ev_stop2;
+  int32_t* stop2_used;
 };
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
 int launch_checksums(const SumParams& p, void* stream);

@@ -61,9 +61,6 @@ constexpr int64_t kMapMinInstances = 4096;
 #ifndef CLSNAP_MAP_PCT
 #define CLSNAP_MAP_PCT 92  // length-ordered slot map when it keeps at most this % of the wave-ticks (A/B knob)
 #endif
-#ifndef CLSNAP_PLAN_KEY
-#define CLSNAP_PLAN_KEY 1  // replay order key: 1 the probe's tick-loop iterations, 0 its final ticks (A/B knob)
-#endif
 #ifndef CLSNAP_LPT
 #define CLSNAP_LPT 1  // slot map order: 1 longest instances first, 0 shortest first (A/B knob)
 #endif
@@ -244,12 +241,28 @@ struct cl_sim {
   // device
   bool dev_ready = false;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;  // per-launch timing events
+  // per-launch timing events: start, stop, and the split replay's spill-capable stop (the
+  // launch time is from start to the later stop)
+  struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr, stop2 = nullptr;
+    int32_t stop2_used = 0;
+  };
+  std::vector<LaunchEvents> ev_pool;
   size_t ev_used = 0;
   double ev_folded_ms = 0;   // time of launches whose events were recycled
   int64_t ev_folded_n = 0;
+  size_t ev_last = 0;        // pool entry of the latest launch (cl_last_kernel_ms)
+
+  int launch_ms(const LaunchEvents& e, float* ms) const {
+    HIP_TRY(hipEventElapsedTime(ms, e.start, e.stop));
+    if (e.stop2_used) {
+      float f2 = 0.f;
+      HIP_TRY(hipEventElapsedTime(&f2, e.start, e.stop2));
+      *ms = std::max(*ms, f2);
+    }
+    return CL_OK;
+  }
 
   // Fold finished launch timings into the accumulator so the event pool stays bounded.
   int fold_events() {
@@ -259,13 +272,13 @@ struct cl_sim {
     if (stream2) HIP_TRY(hipStreamSynchronize(stream2));
     for (size_t i = 0; i < ev_used; ++i) {
       float f = 0.f;
-      HIP_TRY(hipEventElapsedTime(&f, ev_pool[i].first, ev_pool[i].second));
+      int rc = launch_ms(ev_pool[i], &f);
+      if (rc) return rc;
       ev_folded_ms += f;
     }
     ev_folded_n += (int64_t)ev_used;
     if (ev_used) std::swap(ev_pool[0], ev_pool[ev_used - 1]);
-    ev0 = ev_used ? ev_pool[0].first : ev0;
-    ev1 = ev_used ? ev_pool[0].second : ev1;
+    ev_last = 0;
     ev_used = 0;
     return CL_OK;
   }
@@ -300,7 +313,6 @@ struct cl_sim {
   // bounds 3-4) and the rest the spill-capable one, concurrently on stream2.  Results are per
   // instance and identical on either kernel.
   DevBuf<uint8_t> d_spill_inst;  // [n_inst] probe: 1 where a push spilled to HBM
-  DevBuf<int32_t> d_iters;       // [n_inst] probe: tick-loop iterations (idle ticks folded)
   int64_t plan_ops = -1;         // program length the plan holds for (-1: none)
   int64_t plan_tried = -1;       // program length a probe last ran for
   bool probe = false;            // the last launch was a probe (plan built at the next sync)
@@ -358,15 +370,16 @@ struct cl_sim {
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
-      d_ovh.release(); d_spill_inst.release(); d_iters.release(); d_map.release(); d_hist.release(); d_sums.release();
+      d_ovh.release(); d_spill_inst.release(); d_map.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       d_pk_tok.release(); d_pk_done.release(); d_pk_msg.release(); d_pk_cnt.release(); d_pk_bsum.release();
       d_pk_off.release(); d_rec2.release();
       for (auto& e : pk_ev)
         if (e) (void)hipEventDestroy(e);
       for (auto& e : ev_pool) {
-        (void)hipEventDestroy(e.first);
-        (void)hipEventDestroy(e.second);
+        (void)hipEventDestroy(e.start);
+        (void)hipEventDestroy(e.stop);
+        (void)hipEventDestroy(e.stop2);
       }
       if (stream2) (void)hipStreamDestroy(stream2);
       if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -572,7 +585,6 @@ struct cl_sim {
     if ((rc = d_ovf.ensure(ov))) return rc;
     if ((rc = d_ovh.ensure(lay.ocap_log2 >= 0 ? (size_t)std::max(C, 1) * stride : 1))) return rc;
     if (lay.ocap_log2 >= 0 && (rc = d_spill_inst.ensure((size_t)n_inst))) return rc;
-    if ((rc = d_iters.ensure((size_t)n_inst))) return rc;
     plan_ops = plan_tried = -1;
     need_fresh = true;
     return CL_OK;
@@ -711,7 +723,6 @@ struct cl_sim {
       HIP_TRY(hipMemsetAsync(d_spill_inst.p, 0, (size_t)n_inst, stream));
       p.spill_flag = d_spill_inst.p;
     }
-    if (probe && CLSNAP_SKIP) p.iters = d_iters.p;
     if (p.split_slot > 0 && !stream2) {
       HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
@@ -719,27 +730,29 @@ struct cl_sim {
     }
     if (ev_used == 256 && (rc = fold_events())) return rc;
     if (ev_used == ev_pool.size()) {
-      std::pair<hipEvent_t, hipEvent_t> pr;
-      HIP_TRY(hipEventCreateWithFlags(&pr.first, hipEventDisableSystemFence));  // timing only: no cache writeback per record
-      HIP_TRY(hipEventCreateWithFlags(&pr.second, hipEventDisableSystemFence));
-      ev_pool.push_back(pr);
+      LaunchEvents le;  // timing only: no cache writeback per record
+      HIP_TRY(hipEventCreateWithFlags(&le.start, hipEventDisableSystemFence));
+      HIP_TRY(hipEventCreateWithFlags(&le.stop, hipEventDisableSystemFence));
+      HIP_TRY(hipEventCreateWithFlags(&le.stop2, hipEventDisableSystemFence));
+      ev_pool.push_back(le);
     }
+    ev_last = ev_used;
     auto& pr = ev_pool[ev_used++];
+    pr.stop2_used = 0;
     // the dispatch records both events (the kernel's own start/end timestamps): two
     // hipEventRecord packets around it cost 0.7 us more per launch (C2 0.1816 -> 0.1809 ms per
     // step) and bracketed ~1 us of packet processing into the kernel time
     const bool pipe = CLSNAP_PIPE && planned && p.split_slot > 0 && p.split_slot < n_inst && stream2 && !save_state;
     if (!pipe && (rc = join_stream2())) return rc;
     int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p,
-                        ExecLaunch{stream, pr.first, pr.second, stream2, ev_fork, ev_join,
-                                   pipe && CLSNAP_PIPE == 1 ? (s_dirty ? 1 : 0) : 1, pipe ? 0 : 1});
+                        ExecLaunch{stream, pr.start, pr.stop, stream2, ev_fork, ev_join,
+                                   pipe && CLSNAP_PIPE == 1 ? (s_dirty ? 1 : 0) : 1, pipe ? 0 : 1, pr.stop2,
+                                   &pr.stop2_used});
     if (pipe) {
       s2_live = true;
       s_dirty = false;
     }
     if (e != 0) return set_err(CL_E_DEVICE, "exec kernel launch failed: %s", hipGetErrorString((hipError_t)e));
-    ev0 = pr.first;
-    ev1 = pr.second;
     timed = true;
     executed = (int32_t)ops.size();
     need_fresh = false;
@@ -758,6 +771,13 @@ struct cl_sim {
   int sync() {
     if (!dev_ready) return CL_OK;
     HIP_TRY(hipSetDevice(device));
+    // a pipelined replay's stream2 half (s2_live) writes results too: `stream` waits for it
+    // first, whichever path reached here (cl_wait_snapshot took the lock without
+    // SIM_CHECK and could read snap_tick while the spill-capable half still ran)
+    if (s2_live) {
+      const int jrc = join_stream2();
+      if (jrc) return jrc;
+    }
     HIP_TRY(hipStreamSynchronize(stream));
     if (probe) {
       probe = false;
@@ -784,14 +804,10 @@ struct cl_sim {
     plan_tried = probe_ops;
     plan_map = plan_nospill = false;
     plan_split = plan_spilled = 0;
-    // the length of an instance's replay: its tick-loop iterations (the final tick counts the
-    // idle ticks the kernel folds; CLSNAP_PLAN_KEY 0 sorts by it anyway, an A/B knob)
+    // the length of an instance's replay: its final tick (one tick-loop iteration per tick)
     std::vector<int32_t> t((size_t)n_inst);
-    if (CLSNAP_SKIP && CLSNAP_PLAN_KEY && d_iters.p)
-      HIP_TRY(hipMemcpy(t.data(), d_iters.p, t.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
-    else
-      HIP_TRY(hipMemcpy2D(t.data(), sizeof(int32_t), d_regs.p + R_TIME, R_NUM * sizeof(int32_t), sizeof(int32_t),
-                          t.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy2D(t.data(), sizeof(int32_t), d_regs.p + R_TIME, R_NUM * sizeof(int32_t), sizeof(int32_t),
+                        t.size(), hipMemcpyDeviceToHost));
     std::vector<uint8_t> sp((size_t)n_inst, 0);
     if (probe_flags) HIP_TRY(hipMemcpy(sp.data(), d_spill_inst.p, sp.size(), hipMemcpyDeviceToHost));
     std::vector<int32_t> clean, spilled, ident((size_t)n_inst);
@@ -1264,7 +1280,9 @@ int cl_flush(cl_sim* sim) {
 
 int cl_rerun(cl_sim* sim) {
   SIM_CHECK_NOJOIN(sim);
-  return sim->launch(true, false);
+  const int rc = sim->launch(true, false);
+  if (rc == CL_OK) sim->notify_waiters();  // a blocked collector re-checks against the new run
+  return rc;
 }
 
 int cl_replay_spill_free(cl_sim* sim, int32_t* on) {
@@ -1322,7 +1340,7 @@ int cl_last_kernel_ms(cl_sim* sim, double* ms) {
   int rc = sim->sync();
   if (rc) return rc;
   float f = 0.f;
-  HIP_TRY(hipEventElapsedTime(&f, sim->ev0, sim->ev1));
+  if ((rc = sim->launch_ms(sim->ev_pool[sim->ev_last], &f))) return rc;
   *ms = f;
   return CL_OK;
 }
@@ -1491,6 +1509,11 @@ int cl_wait_snapshot(cl_sim* sim, int32_t sid, int64_t inst_lo, int64_t inst_hi,
   } waiting(sim);
   for (;;) {
     if (sim->closing) return set_err(CL_E_STATE, "the sim is being destroyed");
+    // (the driver thread may have issued a pipelined replay since the last wake-up)
+    if (sim->s2_live) {
+      const int jrc = sim->join_stream2();
+      if (jrc) return jrc;
+    }
     int64_t n = 0, frozen = 0;
     int rc = sim->count_complete(sid, inst_lo, inst_hi, &n, &frozen);
     if (rc) return rc;

@@ -164,11 +164,6 @@ using InLinks = uint32_t[unrolled(D) ? D : 1];
 #ifndef CLSNAP_CURREG
 #define CLSNAP_CURREG 1
 #endif
-// Phase A stores only the popped link's head word (one store at a runtime offset) instead of
-// one predicated store per out-link (A/B knob).
-#ifndef CLSNAP_POPW
-#define CLSNAP_POPW 0
-#endif
 // Out-link head words (8-bit ring head, 8-bit count) of the unrolled kernels in two packed
 // registers instead of the link words' lo16 halves (A/B knob): phase A's and the pushes' LDS
 // reads + writes become register ops; the halves are refreshed for the epilogue.
@@ -399,41 +394,17 @@ __device__ __forceinline__ void refill(const Ctx& x, int32_t ko, uint32_t slot) 
   *hp = (h + 1) & om;
 }
 
-// Minimum of v over this lane's instance segment (lanes seg_base .. seg_base + N - 1).
-__device__ __forceinline__ uint32_t seg_min(const Ctx& x, uint32_t v) {
-  const int32_t N = x.p.n_nodes;
-  if (N <= 16 && (N & (N - 1)) == 0) {  // aligned power-of-two segments: DPP butterflies
-    if (N >= 2) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
-    if (N >= 4) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
-    if (N >= 8) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
-    if (N >= 16) v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false)); // row_mirror
-    return v;
-  }
-  // any N: suffix minimum inside the segment, then the segment head's value
-  const int32_t last = x.seg_base + N - 1;
-  for (int32_t d = 1; d < N; d <<= 1) v = min(v, (uint32_t)__shfl((int)v, min(x.lane + d, last)));
-  return (uint32_t)__shfl((int)v, x.seg_base);
-}
-
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
 // Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
-// it[] holds this node's in-link words.  `lim` (>= 1 when act): the ticks the caller may
-// still run.  Returns the reference ticks this call advanced the instance by (0 when !act):
-// idle ticks folded in front of the delivering one, or lim when all of them are idle.
+// it[] holds this node's in-link words.
 template <int D, bool STAGED, bool TRACE>
-__device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act, int32_t lim) {
+__device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
   const unsigned long long pt0 = PROF_T();
   ln.time += act ? 1 : 0;
-  int32_t adv = act ? 1 : 0;
-  // earliest head receiveTime over the lane's non-empty out-links not popped (idle folding)
-  uint32_t mrt = 0x7fffffffu;
-  const uint32_t peek0 = ln.peek;
-  bool anyq = false;  // (CLSNAP_SKIP 2) a non-empty out-link at tick start
   // ---- A: pick ------------------------------------------------------------
   uint32_t pick = 0, empty_scanned = 0;
-  uint32_t pw_val = 0;  // (CLSNAP_POPW) the popped link's new head word
   if constexpr (unrolled(D) && CLSNAP_A_PRED) {
     bool scanning = act;
 #pragma unroll
@@ -450,18 +421,12 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
       ln.peek += nonempty ? 1u : 0u;
       const uint32_t rt = (e >> 16) & 0x7fffu;
       const bool due = nonempty && (int32_t)rt <= ln.time;
-      if constexpr (CLSNAP_SKIP == 1) mrt = (nonempty && !due) ? min(mrt, rt) : mrt;
-      if constexpr (CLSNAP_SKIP == 2) anyq = anyq || nonempty;
       if (__builtin_expect(due && cnt > cap, 0)) refill(x, ko, slot);
       const uint32_t popped = ((cnt - 1) << 8) + ((head + 1) & (cap - 1));
-      if constexpr (CLSNAP_POPW) pw_val = due ? popped : pw_val;
-      else hw_set<D>(x, ln, ko, due ? popped : chw);
+      hw_set<D>(x, ln, ko, due ? popped : chw);
       pick = due ? ((e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16)) : pick;
       scanning = scanning && !due;
     }
-    // (CLSNAP_POPW) one head-word store, the popped link's, at its runtime column offset
-    if constexpr (CLSNAP_POPW)
-      if (pick & kPickValid) PH(lay.w_lnk + ((pick >> 16) & 0x7fu), 0) = (uint16_t)pw_val;
   } else if (act) {
     bool done = false;
 #pragma unroll
@@ -478,11 +443,7 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
       const uint32_t head = chw & (cap - 1);
       const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + head;
       const uint32_t e = PW(slot);
-      if constexpr (CLSNAP_SKIP == 2) anyq = true;
-      if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) {
-        if constexpr (CLSNAP_SKIP == 1) mrt = min(mrt, (e >> 16) & 0x7fffu);
-        continue;
-      }
+      if ((int32_t)((e >> 16) & 0x7fffu) > ln.time) continue;
       if (__builtin_expect(cnt > cap, 0)) refill(x, ko, slot);
       hw_set<D>(x, ln, ko, ((cnt - 1) << 8) + ((head + 1) & (cap - 1)));
       pick = (e & (kMarkerBit | 0xffffu)) | kPickValid | ((uint32_t)ko << 16);
@@ -492,32 +453,6 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
   XW(lay.x_pick + x.lane) = pick;
   // Queue.Pop (sim.go:85), counted at the sender: at most one per tick, so 16 bits each
   ln.pops += (pick & kPickValid) ? ((pick & kMarkerBit) ? 0x10000u : 1u) : 0u;
-  if constexpr (CLSNAP_SKIP == 2) {
-    // An instance whose queues are all empty at tick start delivers nothing in any tick
-    // the caller still allows (no events run inside the loop): they are all folded here.
-    const bool empty = act && seg_min(x, anyq ? 0u : 1u) != 0;
-    if (__ballot(empty) && empty) {
-      ln.time += lim - 1;
-      adv = lim;
-    }
-  }
-  if constexpr (CLSNAP_SKIP == 1) {
-    // An instance none of whose senders popped is idle until its earliest head comes due:
-    // the ticks before it only peek every non-empty out-link once more, so they are folded
-    // into this iteration (up to the lim - 1 ticks the caller still allows after this one).
-    const int32_t N = x.p.n_nodes;
-    const uint64_t segm = N == 64 ? ~0ull : (((1ull << N) - 1) << x.seg_base);
-    const bool idle = act && (__ballot((pick & kPickValid) != 0) & segm) == 0;
-    if (__ballot(idle)) {
-      const int32_t smin = (int32_t)seg_min(x, mrt);
-      if (idle) {
-        const int32_t more = min(smin - ln.time, lim) - 1;  // idle ticks after this one
-        ln.peek += (uint32_t)more * (ln.peek - peek0);
-        ln.time += more;
-        adv += more;
-      }
-    }
-  }
   wave_sync();
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
@@ -594,7 +529,6 @@ __device__ __forceinline__ int32_t tick(const Ctx& x, Lane& ln, const InLinks<D>
 #if CLSNAP_PROF
   ln.prof[7] += 1;
 #endif
-  return adv;
 }
 
 // SendTokens (node.go:112-131) of one send event: balance check, link lookup, push -- all
@@ -815,7 +749,6 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   wave_sync();
   ln.alive = valid && ln.status == ST_OK;
   int32_t n_started = p.n_started_before;
-  uint32_t nit = 0;  // (idle folding) tick-loop iterations this instance was active in, for the probe
 #if CLSNAP_PROF
   PROF_ADD(ln, 5, pro0);
 #endif
@@ -855,23 +788,21 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
       // TICK: op.a ticks.  DRAIN: tick until every started snapshot completed (at most
       // op.a ticks, else HANG), then op.b more (test_common.go:123-137).  Per instance.
       const bool drain = op.kind == OP_DRAIN;
-      // (rem: ticks left to run; dt: waiting ticks run, per lane -- folded idle ticks count)
-      // (without folding every waiting lane runs one tick per iteration: the uniform loop count)
-      int32_t rem = drain ? op.b : op.a, dt = 0;
+      // (rem: ticks left to run after the wait; every waiting lane runs one tick per
+      // iteration, so the iteration count is its waiting ticks)
+      int32_t rem = drain ? op.b : op.a;
       bool waiting = drain;
       for (int32_t iter = 0;; ++iter) {
         if (waiting && (!ln.alive || (int32_t)XW(lay.x_ndone + seg) >= n_started)) waiting = false;
-        if (waiting && (CLSNAP_SKIP ? dt : iter) >= op.a) {
+        if (waiting && iter >= op.a) {
           ln.status = ST_HANG;
           ln.alive = false;
           waiting = false;
         }
         const bool act = ln.alive && (waiting || rem > 0);
         if (!__ballot(act)) break;
-        if constexpr (CLSNAP_SKIP) nit += act ? 1u : 0u;
-        const int32_t adv = tick<D, STAGED, TRACE>(x, ln, it, act, waiting ? op.a - (CLSNAP_SKIP ? dt : iter) : rem);
-        if (CLSNAP_SKIP && waiting) dt += adv;
-        else if (!waiting) rem -= adv;
+        tick<D, STAGED, TRACE>(x, ln, it, act);
+        if (act && !waiting) rem--;
       }
 #if CLSNAP_PROF
       PROF_ADD(ln, 4, ot0);
@@ -939,7 +870,6 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
     r[R_POP_MK] = (int32_t)acc[2];
     r[R_PUSH] = (int32_t)acc[3];
     r[R_INFLIGHT_TOK] = (int32_t)acc[4];
-    if (CLSNAP_SKIP && p.iters) p.iters[ii] = (int32_t)nit;
   }
   if (!p.save_state) return;
   if constexpr (cur_reg(D)) {  // the link words' cursor halves, for the state image
@@ -1224,20 +1154,24 @@ int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, 
   b.slot_base = (uint32_t)p.split_slot;
   ExecLaunch la = L;
   la.ev_stop = nullptr;
+  // the spill-capable dispatch records a stop event of its own (ev_stop2): unjoined, it may
+  // end after the main stream's stop, and the launch time is the later of the two
+  ExecLaunch lb = L;
+  lb.ev_stop = L.ev_stop2;
   int e;
   if (CLSNAP_SPILL_FIRST) {
     // the spilling instances are the longest: their kernel is dispatched first so its
     // workgroups are resident from the start instead of queueing behind the main grid (the
     // tail of a small per-GPU batch); it records the start event
-    ExecLaunch lb = L;
-    lb.ev_stop = nullptr;
     if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
     la.ev_start = nullptr;
     if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
   } else {
     if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
-    if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, L, s2))) return e;
+    lb.ev_start = nullptr;
+    if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
   }
+  if (L.stop2_used && L.ev_stop2) *L.stop2_used = 1;
   if (!L.join) {  // replays back to back: the main stream does not wait for stream2 (cl_host.cpp)
     if (L.ev_stop && (he = hipEventRecord((hipEvent_t)L.ev_stop, s))) return (int)he;
     return 0;
