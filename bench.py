@@ -52,7 +52,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 # traffic and snapshot-placement seeds ("replicas only").
 GRAPH_CONFIGS = {
     "c4": dict(kind="regular", n=1 << 20, degree=8, tokens=100, steps=80, snap_steps=[5], fifo=16,
-               seed=20240,
+               seed=20240, cpu_full=True,
                desc="random 8-out regular digraph, 2^20 nodes, one snapshot under continuous token "
                     "traffic (p=1/4 per node per tick), 80 ticks"),
     "c5": dict(kind="powerlaw", n=100_000, targets=8, exponent=0.9, ring=True, tokens=100, steps=4100,
@@ -652,15 +652,21 @@ def cpu_baseline_graph(g, cfg, n, steps, snap_steps, snap_nodes, rs, budget_s):
         c = o.counters()
         return secs, c["pop_tok"] + c["pop_mk"], o.status
 
-    k = min(steps, 8)
-    secs, pk, st = run(k)
-    while secs < budget_s / 3 and k < steps:   # later ticks cost more (longer logs): grow
-        k = min(steps, 2 * k)
+    if cfg.get("cpu_full"):
+        # the whole program (C4: 80 ticks, ~25 s of oracle time): the same run the GPU times
+        k = steps
         secs, pk, st = run(k)
+    else:
+        k = min(steps, 8)
+        secs, pk, st = run(k)
+        while secs < budget_s / 3 and k < steps:   # later ticks cost more (longer logs): grow
+            k = min(steps, 2 * k)
+            secs, pk, st = run(k)
+    what = f"all {steps} ticks" if k == steps else f"first {k} of {steps} ticks"
     return {"value": pk / secs, "unit": "packets/s", "cores": 1, "kind": "port",
-            "sample": f"first {k} of {steps} ticks of the same graph and program ({pk} packets, "
-                      f"{secs:.1f} s); CPU restatement in C (oracle/cl_oracle.c), one simulation on one "
-                      f"thread -- not the Go reference (no Go toolchain in the image)"}
+            "sample": f"{what} of the same graph and program ({pk} packets, {secs:.1f} s); CPU restatement in "
+                      f"C (oracle/cl_oracle.c), one simulation on one thread (the reference simulates one "
+                      f"graph on one goroutine) -- not the Go reference (no Go toolchain in the image)"}
 
 
 def host_cpu():
@@ -700,13 +706,24 @@ def cpu_baseline(top, events, n_total, budget_s):
         total_pkts += int((cnt[ok, 2] + cnt[ok, 3]).sum())
         total_s += secs
         passes += 1
-    return {"value": total_pkts / total_s, "unit": "packets/s", "cores": threads, "kind": "port",
+    rate = total_pkts / total_s
+    return {"value": rate, "unit": "packets/s", "cores": threads, "kind": "port",
             "cpu_model": model, "host_logical_cpus": ncpu,
             "sample": f"{passes} pass(es) over all {n_total} instances of the timed batch (same seeds), "
                       f"{total_s:.1f} s of simulation wall time on {threads} threads; topology and events "
                       f"parsed once outside the timed region; CPU restatement in C (oracle/cl_oracle.c), "
                       f"one simulation per thread at a time -- not the Go reference (no Go toolchain "
-                      f"in the image)"}
+                      f"in the image)",
+            "node_host_estimate": {
+                "value": rate * NODE_GPUS, "unit": "packets/s", "cores": threads * NODE_GPUS,
+                "measured": False,
+                "note": f"the whole 8-GPU node's host share, extrapolated linearly from the measured "
+                        f"{threads}-thread figure (an upper bound): the GPU box grants {threads} host CPUs "
+                        f"per GPU (OMP_NUM_THREADS), and running more threads than that share would take "
+                        f"CPU time from other jobs on the machine ({ncpu} logical CPUs)"}}
+
+
+NODE_GPUS = 8   # MI355X per node (BASELINE.json north_star)
 
 
 if __name__ == "__main__":

@@ -77,6 +77,15 @@ struct PDel {
 
 constexpr uint32_t kEmpty = 0xffffffffu;  // head receiveTime word of an empty channel
 
+// Per-(snapshot, node) state, one 16-byte record at sid * n + v: every marker handling
+// (k_pick's creation bid, k_marker's creation or close, completion) touches one line instead
+// of three arrays' (DESIGN.md §10).
+struct alignas(16) SNode {
+  unsigned long long W;  // creation key: (tick << 32) | creating sender (initiator: | 0xffffffff); ~0 = none
+  int32_t cnt;           // pending accumulator (kBig + links recorded, -1 per later marker)
+  int32_t stok;          // recorded node tokens (CreateLocalSnapshot, node.go:77)
+};
+
 // Device event trace of the graph engine (the reference's debug Logger, logger.go:12-76).
 // One record per LogEvent, appended unordered; the host sorts them into the Logger's order
 // by (epoch, order, sub) and restores LogEvent.nodeTokens by replaying the token changes the
@@ -175,9 +184,7 @@ struct GParams {
   uint32_t* tokcnt;    // [e] by in-position: tokens delivered on the channel so far
   uint32_t* histv;     // [e * hist] by in-position
   // snapshot state
-  uint64_t* W;         // [s_cap * n] creation key: (tick << 32) | creating sender (initiator: | 0xffffffff)
-  int32_t* cnt;        // [s_cap * n] pending accumulator
-  int32_t* stok;       // [s_cap * n] recorded node tokens
+  SNode* sn;           // [s_cap * n] per-(snapshot, node) record: creation key, pending accumulator, node tokens
   uint64_t* rec;       // [s_cap * e] by in-position: recording cursors
   int32_t* done;       // [s_cap] node groups complete (p.done[s_cap..] = gdone)
   int32_t* gdone;      // [s_cap * n_pblocks] nodes complete per group of kGThreads ranks

@@ -173,8 +173,9 @@ struct cl_graph {
   GBuf<long long> d_bsum;
   GBuf<uint32_t> d_histv;
   GBuf<uint64_t> d_hq;
-  GBuf<uint64_t> d_fifo, d_W, d_rec;
-  GBuf<int32_t> d_cnt, d_stok, d_done, d_ctick;
+  GBuf<uint64_t> d_fifo, d_rec;
+  GBuf<SNode> d_sn;
+  GBuf<int32_t> d_done, d_ctick;
   GBuf<GScal> d_sc;
   GBuf<GOp> d_ops;
   GBuf<uint8_t> d_sched;
@@ -208,11 +209,11 @@ struct cl_graph {
     (void)hipStreamSynchronize(stream);
     if (own_stream != stream) (void)hipStreamSynchronize(own_stream);
     GBuf<int32_t>* i32s[] = {&d_out_off, &d_in_off, &d_in_src, &d_init_tok, &d_tokens,
-                             &d_pick,    &d_ltrig,  &d_lsend,    &d_crn,    &d_mcnt,   &d_cnt,      &d_stok,
+                             &d_pick,    &d_ltrig,  &d_lsend,    &d_crn,    &d_mcnt,
                              &d_done,    &d_ctick};
     for (auto* b : i32s) b->release();
     d_cre.release(); d_bsum.release(); d_hq.release(); d_histv.release(); d_mlist.release(); d_route.release();
-    d_tokcnt.release(); d_ppay.release(); d_in_oj.release(); d_fifo.release(); d_W.release(); d_rec.release(); d_sc.release(); d_ops.release();
+    d_tokcnt.release(); d_ppay.release(); d_in_oj.release(); d_fifo.release(); d_sn.release(); d_rec.release(); d_sc.release(); d_ops.release();
     d_sched.release(); d_scratch.release(); d_big.release(); d_cpart.release();
     d_trace.release(); d_trace_cnt.release();
     d_outbox.release(); d_inbox.release(); d_out_n.release(); d_rmlist.release(); d_reports.release();
@@ -468,8 +469,8 @@ struct cl_graph {
         (rc = d_mcnt.ensure(NP)) || (rc = d_big.ensure(N)) || (rc = d_cpart.ensure((size_t)kParts * kNumCnt)) ||
         (rc = d_cre.ensure(E)) || (rc = d_bsum.ensure(2 * NP)) || (rc = d_hq.ensure(E)) ||
         (rc = d_tokcnt.ensure(E)) || (rc = d_ppay.ensure(N)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
-        (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_W.ensure(s_cap * N)) ||
-        (rc = d_rec.ensure(s_cap * E)) || (rc = d_cnt.ensure(s_cap * N)) || (rc = d_stok.ensure(s_cap * N)) ||
+        (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_sn.ensure(s_cap * N)) ||
+        (rc = d_rec.ensure(s_cap * E)) ||
         (rc = d_done.ensure((size_t)s_cap * (1 + NP))) || (rc = d_ctick.ensure(s_cap)) || (rc = d_sc.ensure(1)) ||
         (rc = d_scratch.ensure(3 + (size_t)s_cap)))
       return rc;
@@ -536,9 +537,7 @@ struct cl_graph {
     p.ppay = d_ppay.p;
     p.in_oj = d_in_oj.p;
     p.histv = d_histv.p;
-    p.W = d_W.p;
-    p.cnt = d_cnt.p;
-    p.stok = d_stok.p;
+    p.sn = d_sn.p;
     p.rec = d_rec.p;
     p.done = d_done.p;
     p.gdone = d_done.p + s_cap;
@@ -1238,7 +1237,9 @@ int cl_graph_debug_poison_outputs(cl_graph* g) {
   if (!g->dev_ready || !g->d_tokens.p) return CL_OK;
   GHIP(hipSetDevice(g->device));
   GHIP(hipMemsetAsync(g->d_tokens.p, 0xA5, g->d_tokens.bytes(), g->stream));
-  GHIP(hipMemsetAsync(g->d_stok.p, 0xA5, g->d_stok.bytes(), g->stream));
+  // (the whole record plane: the run's reset rewrites W and cnt, so stok stays poisoned
+  // wherever the run creates no local snapshot)
+  GHIP(hipMemsetAsync(g->d_sn.p, 0xA5, g->d_sn.bytes(), g->stream));
   GHIP(hipMemsetAsync(g->d_rec.p, 0xA5, g->d_rec.bytes(), g->stream));
   GHIP(hipMemsetAsync(g->d_ctick.p, 0xA5, g->d_ctick.bytes(), g->stream));
   GHIP(hipMemsetAsync(g->d_cpart.p, 0xA5, g->d_cpart.bytes(), g->stream));
@@ -1276,8 +1277,7 @@ int cl_graph_device_bytes(cl_graph* g, int64_t* bytes) {
        g->d_ltrig.bytes() + g->d_lsend.bytes() + g->d_crn.bytes() + g->d_mlist.bytes() + g->d_mcnt.bytes() +
        g->d_big.bytes() + g->d_cpart.bytes() +
        g->d_cre.bytes() + g->d_bsum.bytes() + g->d_hq.bytes() +
-       g->d_histv.bytes() + g->d_fifo.bytes() + g->d_W.bytes() + g->d_rec.bytes() +
-       g->d_cnt.bytes() + g->d_stok.bytes() + g->d_done.bytes() + g->d_ctick.bytes() + g->d_sched.bytes();
+       g->d_histv.bytes() + g->d_fifo.bytes() + g->d_sn.bytes() + g->d_rec.bytes() + g->d_done.bytes() + g->d_ctick.bytes() + g->d_sched.bytes();
   *bytes = (int64_t)b;
   return CL_OK;
 }
@@ -1342,7 +1342,9 @@ int cl_graph_collect_snapshot(cl_graph* g, int32_t sid, int64_t* tokens, int64_t
   const size_t N = (size_t)g->n, E = (size_t)g->e;
   if (tokens) {
     std::vector<int32_t> st(N);
-    GHIP(hipMemcpy(st.data(), g->d_stok.p + (size_t)sid * N, N * sizeof(int32_t), hipMemcpyDeviceToHost));
+    // (the stok word of each 16-byte record of the plane: one strided copy)
+    GHIP(hipMemcpy2D(st.data(), sizeof(int32_t), &g->d_sn.p[(size_t)sid * N].stok, sizeof(SNode), sizeof(int32_t), N,
+                     hipMemcpyDeviceToHost));
     for (size_t v = 0; v < N; ++v) tokens[v] = st[v];
   }
   if (!msg_offsets) return CL_OK;

@@ -335,6 +335,15 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
   if (i < (size_t)p.s_cap) p.ctick[i] = -1;
 }
 
+// Per-(snapshot, node) records: W = ~0 (no creation), cnt = 0; stok is left as it is (written
+// at creation; a poisoned plane stays poisoned where a run writes nothing).  One 12-byte store.
+__global__ void __launch_bounds__(kGThreads) k_sn_reset(SNode* sn, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint3* w = reinterpret_cast<uint3*>(&sn[i]);
+    *w = make_uint3(0xffffffffu, 0xffffffffu, 0u);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // tick phase A: pick + deliver
 // ---------------------------------------------------------------------------
@@ -417,7 +426,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
              (int32_t)(pay & kGPayload));
       if (pay & kGMarker) {
         const int32_t sid = (int32_t)(pay & kGPayload);
-        atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + v], ((unsigned long long)t << 32) | (uint32_t)s);
+        atomicMin(&p.sn[(size_t)sid * p.n + v].W, ((unsigned long long)t << 32) | (uint32_t)s);
         p.mlist[bk * kGThreads + atomicAdd(&s_m, 1)] = MDel{s, v, k, sid};
       } else {
         atomicAdd(&p.tokens[v], (int32_t)pay);  // HandleToken node.go:175
@@ -489,7 +498,8 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
     sid = m.sid;
     vdone = v;
     const size_t sv = (size_t)sid * p.n + v;
-    const uint64_t key = p.W[sv];
+    SNode* rn = &p.sn[sv];
+    const uint64_t key = rn->W;
     const int32_t lo = p.in_off[v], hi = p.in_off[v + 1];
     if (key == (((uint64_t)t << 32) | (uint32_t)s0)) {
       // first marker: CreateLocalSnapshot(src) + SendToNeighbors (node.go:153-156)
@@ -504,13 +514,13 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
       // (both returning atomics issued before either result is used: one round trip)
       const int add = kBig + (hi - lo) - 1;
       const int slot = atomicAdd(&p.crn[v], 1);
-      const int cold = atomicAdd(&p.cnt[sv], add);
+      const int cold = atomicAdd(&rn->cnt, add);
       p.cre[lo + slot] = ((uint64_t)(uint32_t)s0 << 32) | (uint32_t)sid;
       bx = BigX{lo, hi, s0, sid, k, v, {0, 0}};
       if (hi - lo <= kSmallIndeg) {
         cslot = 0;  // numbered below
       } else {
-        p.stok[sv] = p.tokens[v];  // k_push's expansion subtracts the later same-tick tokens
+        rn->stok = p.tokens[v];  // k_push's expansion subtracts the later same-tick tokens
         bslot = atomicAdd(&s_nb, 1);
       }
       done = cold + add == kBig;
@@ -522,7 +532,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
         c[0] += e - r[0];
         r[1] = e;
       }  // else created this tick by a lower-ranked sender: its expansion closes it
-      done = atomicAdd(&p.cnt[sv], -1) - 1 == kBig;
+      done = atomicAdd(&rn->cnt, -1) - 1 == kBig;
     }
   }
   if (done && p.trace) {  // EndSnapshotRecord (sim.go:127); the host moves it behind the last marker
@@ -555,7 +565,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
     if (ts) atomicAdd(&s_ctsum[lo], ts);
   }
   __syncthreads();
-  if (cslot >= 0) p.stok[(size_t)bx.sid * p.n + bx.v] = p.tokens[bx.v] - s_ctsum[cslot];
+  if (cslot >= 0) p.sn[(size_t)bx.sid * p.n + bx.v].stok = p.tokens[bx.v] - s_ctsum[cslot];
   if (threadIdx.x == 0 && s_nb) s_base = atomicAdd(&p.sc->big_n, s_nb);
   if (!p.part) tally(p, bk, s_trig[threadIdx.x], sendbit);  // (has a barrier: s_base is final below)
   else __syncthreads();
@@ -952,7 +962,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
       const BigX x = sx[lo];
       const int32_t k = x.lo + (int32_t)(w - spre[lo]);
       const int tsum = expand_range(p, t, x.s0, x.sid, x.karr, k, k + 1, 1);
-      if (tsum) atomicSub(&p.stok[(size_t)x.sid * p.n + x.v], tsum);
+      if (tsum) atomicSub(&p.sn[(size_t)x.sid * p.n + x.v].stok, tsum);
     }
   }
 }
@@ -1013,9 +1023,9 @@ __global__ void __launch_bounds__(kGThreads) k_hostops(GParams p, int32_t time, 
         for (int32_t j = 0; j < od && p.trace; ++j)  // SendToNeighbors (node.go:100)
           gtrace(p, time, kTrHost, (uint32_t)(ob + i), 1u + (uint32_t)j, TK_SENT_MARKER, v, p.route[obv + j].x, sid);
         const size_t sv = (size_t)sid * p.n + v;
-        p.W[sv] = ((uint64_t)(uint32_t)time << 32) | 0xffffffffull;
-        p.stok[sv] = p.tokens[v];
-        atomicAdd(&p.cnt[sv], kBig + (hi - lo));
+        p.sn[sv].W = ((uint64_t)(uint32_t)time << 32) | 0xffffffffull;
+        p.sn[sv].stok = p.tokens[v];
+        atomicAdd(&p.sn[sv].cnt, kBig + (hi - lo));
         s_draw = p.sc->draw;
       }
       __syncthreads();
@@ -1100,7 +1110,7 @@ __device__ inline void apply_delivery(const GParams& p, int32_t t, const PDel d)
   p.ppay[d.s] = d.pay;
   if (d.pay & kGMarker) {
     const int32_t sid = (int32_t)(d.pay & kGPayload);
-    atomicMin((unsigned long long*)&p.W[(size_t)sid * p.n + d.v], ((unsigned long long)t << 32) | (uint32_t)d.s);
+    atomicMin(&p.sn[(size_t)sid * p.n + d.v].W, ((unsigned long long)t << 32) | (uint32_t)d.s);
     p.rmlist[atomicAdd(&p.out_n[1], 1u)] = MDel{d.s, d.v, d.k, sid};
   } else {
     atomicAdd(&p.tokens[d.v], (int32_t)d.pay);
@@ -1253,7 +1263,8 @@ __global__ void k_finish(GParams p, int32_t n_sids, unsigned long long* out) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int32_t sid = (int32_t)(i / span), v = p.part_lo + (int32_t)(i % span);
     const size_t sv = (size_t)sid * p.n + v;
-    if (p.W[sv] == ~0ull || p.cnt[sv] == kBig) continue;
+    const SNode r0 = p.sn[sv];
+    if (r0.W == ~0ull || r0.cnt == kBig) continue;
     const uint64_t* r = p.rec + (size_t)sid * p.e;
     for (int32_t k = p.in_off[v]; k < p.in_off[v + 1]; ++k) {
       const uint64_t x = r[k];
@@ -1296,9 +1307,9 @@ __global__ void k_checks_snap(GParams p, int32_t n_sids, unsigned long long* out
   for (int32_t sid = blockIdx.y; sid < n_sids; sid += gridDim.y) {
     if (p.ctick[sid] < 0) continue;
     unsigned long long cut = 0, dig = 0;
-    const int32_t* stok = p.stok + (size_t)sid * p.n;
+    const SNode* sn = p.sn + (size_t)sid * p.n;
     for (size_t v = p.part_lo + gt; v < (size_t)p.part_hi; v += gs) {
-      const int32_t st = stok[v];
+      const int32_t st = sn[v].stok;
       dig += mix64(cg_hash(0x5107ull, (uint64_t)sid, (uint64_t)v) ^ (uint64_t)(uint32_t)st);
       cut += (unsigned long long)(long long)st;
     }
@@ -1325,8 +1336,11 @@ inline int grid_for(int64_t n, int threads = kThreads) { return (int)((n + threa
 int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipError_t e;
-  if ((e = hipMemsetAsync(p.W, 0xff, (size_t)p.s_cap * p.n * sizeof(uint64_t), s))) return e;
-  if ((e = hipMemsetAsync(p.cnt, 0, (size_t)p.s_cap * p.n * sizeof(int32_t), s))) return e;
+  {  // per-(snapshot, node) records: no creation, accumulator 0 (stok is written at creation)
+    const int64_t nsn = (int64_t)p.s_cap * p.n;
+    const int64_t grid = nsn / kThreads + 1 < 65536 ? nsn / kThreads + 1 : 65536;
+    hipLaunchKernelGGL(k_sn_reset, dim3((unsigned)grid), dim3(kThreads), 0, s, p.sn, nsn);
+  }
   if ((e = hipMemsetAsync(p.done, 0, (size_t)p.s_cap * (1 + p.n_pblocks) * sizeof(int32_t), s))) return e;
   if ((e = hipMemsetAsync(p.sc, 0, sizeof(GScal), s))) return e;
   if ((e = hipMemsetAsync(p.cpart, 0, (size_t)kParts * kNumCnt * sizeof(unsigned long long), s))) return e;

@@ -1,0 +1,38 @@
+# Round-4 check of the tree on one GPU (each step under its own limit, chained with set -e):
+#   STEPS (space-separated, default all): launch exec graph abx abg
+#   launch  bench.py --gpus 2 rank launch on the shared device (tests/test_bench_launch.py -m gpu)
+#   exec    batch-engine GPU tests (parity, trace, threaded collect, limits)
+#   vtest   batch-engine parity tests on each variant library of VTESTS
+#   graph   graph-engine GPU tests (graph, graph trace, partition)
+#   abx     interleaved A/B of batch-engine variants (VARIANTS, lib/libclsnap_<v>.so) on CFGS
+#   abg     interleaved A/B of graph-engine variants (GVARIANTS) on C4 and C5
+# usage: TAG=r04a STEPS="exec abx" VARIANTS="hwreg" bash tools/gpu_r04.sh
+set -e
+O=gpurun_out/${TAG:-r04}
+mkdir -p $O
+PYT="python -u -m pytest -x -q --timeout 280 --timeout-method thread -m gpu"
+for s in ${STEPS:-launch exec graph abx abg}; do
+  case $s in
+    launch) timeout -k 10 400 $PYT tests/test_bench_launch.py > $O/pytest_launch.log 2>&1 ;;
+    exec) timeout -k 10 900 $PYT tests/test_gpu_parity.py tests/test_trace_gpu.py tests/test_threaded_collect.py \
+            tests/test_gpu_limits.py > $O/pytest_exec.log 2>&1 ;;
+    vtest) for v in ${VTESTS}; do
+             CLSNAP_VARIANT=$v timeout -k 10 900 $PYT tests/test_gpu_parity.py -k "not random_scenarios" > $O/pytest_var_$v.log 2>&1
+           done ;;
+    graph) timeout -k 10 900 $PYT tests/test_graph_gpu.py tests/test_graph_trace_gpu.py tests/test_partition_gpu.py \
+            > $O/pytest_graph.log 2>&1 ;;
+    abx) for r in 1 2; do for v in base ${VARIANTS}; do
+           if [ $v = base ]; then VAR=""; else VAR=$v; fi
+           for c in ${CFGS:-c3 c2}; do
+             CLSNAP_VARIANT=$VAR timeout -k 10 200 python -u bench.py --config $c --steps 50 --warmup 5 \
+               --no-cpu-baseline --no-collect ${EXTRA} > $O/abx_${v}_${c}_$r.log 2>&1
+           done; done; done ;;
+    abg) for r in 1 2; do for v in base ${GVARIANTS}; do
+           if [ $v = base ]; then VAR=""; else VAR=$v; fi
+           for c in ${GCFGS:-c4 c5}; do
+             CLSNAP_VARIANT=$VAR timeout -k 10 300 python -u bench.py --config $c --steps 3 --warmup 1 \
+               --no-cpu-baseline > $O/abg_${v}_${c}_$r.log 2>&1
+           done; done; done ;;
+  esac
+  echo "step $s done" >> $O/steps.log
+done
