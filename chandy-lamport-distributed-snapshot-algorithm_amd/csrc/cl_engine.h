@@ -11,8 +11,7 @@ enum OpKind : int32_t {
   OP_SEND = 1,   // a = src rank, b = out-index at src (-1: unknown dest), c = tokens  (node.go:112-131)
   OP_SNAP = 2,   // a = node rank, b = snapshot id, c = outdeg(a)                   (sim.go:105-123)
   OP_TICK = 3,   // a = number of ticks                                      (sim.go:71-95)
-  OP_DRAIN = 4,  // a = max drain ticks, b = extra ticks (maxDelay+1),       (test_common.go:123-137)
-                 // c = snapshots started before it (device program; refill mode)
+  OP_DRAIN = 4,  // a = max drain ticks, b = extra ticks (maxDelay+1)        (test_common.go:123-137)
   OP_SENDS = 5,  // a = k: the next k ops are OP_SENDs from pairwise distinct senders, run
                  // as one lane-parallel step (device program only; built by the host from
                  // runs of consecutive sends, e.g. one event-file line per node)
@@ -126,10 +125,6 @@ struct Layout {
   int32_t w_fifo, w_lnk, w_int, w_pend, w_trig, priv;
   // shared region (words, after the 64 private columns)
   int32_t x_pick, x_tslot, x_off, x_done, x_ndone, x_acc;
-  // refill mode (cl_kernels.hip exec_refill): per segment two words of program state, then
-  // three words of the wave's work queue; in segment-completion mode (seg_done_mode) they
-  // reuse the completion counters' words, which that mode leaves unused
-  int32_t x_seg, x_q;
   int32_t x_delay_begin;  // words of the shared region zeroed at start (everything before x_delay)
   int32_t x_delay;        // wave's delay rows staged in LDS (0 = not staged; rows read from HBM)
   int32_t shared;
@@ -140,21 +135,6 @@ struct Layout {
   // state image per instance (words): per node priv + G_NUM, then s_cap done counters + ndone
   int32_t state_words;
 };
-
-// Instance completion by a segment-wide AND of the nodes' completed-snapshot masks (DPP) instead
-// of LDS counters (cl_kernels.hip seg_complete; A/B knob): aligned power-of-two instances of at
-// most 16 nodes and at most 16 snapshot ids.
-#ifndef CLSNAP_DPPDONE
-#define CLSNAP_DPPDONE 0
-#endif
-// Full runs that save no state on a persistent grid whose segments pull instances from work
-// counters (cl_kernels.hip exec_refill; A/B knob).
-#ifndef CLSNAP_REFILL
-#define CLSNAP_REFILL 0
-#endif
-inline bool seg_done_mode(int32_t n_nodes, int32_t s_cap) {
-  return CLSNAP_DPPDONE && n_nodes >= 1 && n_nodes <= 16 && (n_nodes & (n_nodes - 1)) == 0 && s_cap <= 16;
-}
 
 // The exec kernel's degree bound for max degree d (cl_kernels.hip launch_exec).
 inline int32_t degree_bound(int32_t d) {
@@ -206,16 +186,6 @@ inline Layout make_layout(int32_t n_nodes, int32_t od, int32_t id, int32_t cap_l
   L.x_ndone = L.x_done + L.ipw * L.sp;
   L.x_acc = L.x_ndone + L.ipw;
   L.x_delay_begin = L.x_acc + 5 * L.ipw;
-  if (seg_done_mode(n_nodes, s_cap) && L.ipw * (L.sp + 1) >= 2 * L.ipw + 3) {
-    L.x_seg = L.x_done;
-    L.x_q = L.x_seg + 2 * L.ipw;
-  } else if (CLSNAP_REFILL) {
-    L.x_seg = L.x_delay_begin;
-    L.x_q = L.x_seg + 2 * L.ipw;
-    L.x_delay_begin = L.x_q + 3;
-  } else {
-    L.x_seg = L.x_q = -1;  // (no refill mode for this layout)
-  }
   const int64_t delay_words = (int64_t)L.ipw * sched_row / 4;  // sched_row is a multiple of 16
   if (sched_row > 0 && delay_words <= delay_budget_words) {
     L.x_delay = (L.x_delay_begin + 3) / 4 * 4;  // 16-byte aligned
@@ -275,11 +245,6 @@ struct ExecParams {
   // slot -> instance for a replay (nullptr: slot i runs instance i).  cl_host orders a
   // replay's instances by their final tick so the segments of a wave finish together
   const int32_t* inst_map;
-  // refill mode (cl_kernels.hip exec_refill; fresh full runs that save no state): a
-  // persistent grid whose segments pull work items from kRefillShards (8) counters, zeroed
-  // before the launch
-  int32_t refill;
-  uint32_t* work;
   // event trace of instances [trace_lo, trace_lo + trace_n) (trace kernel build only)
   TraceRec* trace;          // [trace_n][trace_cap]
   uint32_t* trace_cnt;      // [trace_n] records emitted (may exceed trace_cap: overflow)

@@ -55,7 +55,6 @@ constexpr int32_t kTargetBlocks = 6;
 // Batches of at least this many instances replay through a length-ordered slot map (a few
 // thousand waves: the grouping pays for its one host sort and 4 B per instance of HBM).
 constexpr int64_t kMapMinInstances = 4096;
-constexpr size_t kRefillCounters = 8;  // cl_kernels.hip kRefillShards
 #ifndef CLSNAP_PIPE
 #define CLSNAP_PIPE 2  // split replays back to back: 0 join every replay, 1 neither fork nor join, 2 fork only (A/B knob)
 #endif
@@ -342,7 +341,6 @@ struct cl_sim {
   // wave end their drains together; replays of the same program and delays launch through
   // the map (results are per instance, unchanged).  -1: no map.
   DevBuf<int32_t> d_map;
-  DevBuf<uint32_t> d_work;  // refill mode's work counters (kernel kRefillShards)
   DevBuf<int32_t> d_hist;
   DevBuf<unsigned long long> d_sums;
   // device event trace (cl_trace_enable): instances [trace_lo, trace_lo + trace_n)
@@ -372,7 +370,7 @@ struct cl_sim {
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
-      d_ovh.release(); d_spill_inst.release(); d_map.release(); d_work.release(); d_hist.release(); d_sums.release();
+      d_ovh.release(); d_spill_inst.release(); d_map.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       d_pk_tok.release(); d_pk_done.release(); d_pk_msg.release(); d_pk_cnt.release(); d_pk_bsum.release();
       d_pk_off.release(); d_rec2.release();
@@ -634,12 +632,6 @@ struct cl_sim {
       } else {
         dmap[i] = (int32_t)dops.size();
         dops.push_back(ops[i]);
-        // (refill mode) a drain waits for the snapshots started before it, from op 0
-        if (ops[i].kind == OP_DRAIN) {
-          int32_t ns = 0;
-          for (size_t k = 0; k < i; ++k) ns += ops[k].kind == OP_SNAP;
-          dops.back().c = ns;
-        }
       }
       i = j;
     }
@@ -731,15 +723,6 @@ struct cl_sim {
       HIP_TRY(hipMemsetAsync(d_spill_inst.p, 0, (size_t)n_inst, stream));
       p.spill_flag = d_spill_inst.p;
     }
-    // a full run that saves no state runs on a persistent grid whose segments pull instances
-    // from work counters (cl_kernels.hip exec_refill; the specialized kernels only)
-    if (CLSNAP_REFILL && begin == 0 && !save_state && trace_n == 0 && specialized() && lay.x_seg >= 0 &&
-        refill_program_ok()) {
-      if ((rc = d_work.ensure(kRefillCounters))) return rc;
-      HIP_TRY(hipMemsetAsync(d_work.p, 0, kRefillCounters * sizeof(uint32_t), stream));
-      p.refill = 1;
-      p.work = d_work.p;
-    }
     if (p.split_slot > 0 && !stream2) {
       HIP_TRY(hipStreamCreateWithFlags(&stream2, hipStreamNonBlocking));
       HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
@@ -776,17 +759,6 @@ struct cl_sim {
     state_valid = save_state;  // a rerun leaves no resumable image: the next flush replays
     h_valid = false;
     return CL_OK;
-  }
-
-  // Refill mode keeps a segment's program position, tick count and drain budget in 16-bit
-  // LDS fields (cl_kernels.hip exec_refill).
-  bool refill_program_ok() const {
-    if (dops.size() >= 65536) return false;
-    for (const Op& o : dops)
-      if ((o.kind == OP_TICK && (o.a < 0 || o.a > 65535)) ||
-          (o.kind == OP_DRAIN && (o.a < 0 || o.a > 65535 || o.b < 0 || o.b > 65535 || o.c > 255)))
-        return false;
-    return true;
   }
 
   // The launcher's specialized kernels (and so split replays) serve this layout: unrolled

@@ -72,7 +72,6 @@ struct Ctx {
   uint32_t nod_plane;  // bytes per sid plane of the node records (uniform)
   int32_t draws;       // delays per instance, clamped to int32 (draw indices are int32)
   bool mul24;  // every plane offset sid * plane fits the 24-bit multiplier
-  bool dpp_done;  // instance completion by segment AND (CLSNAP_DPPDONE, aligned power-of-two N <= 16)
 };
 
 // Byte offset of snapshot plane `sid` (sid < 32).  v_mul_u32_u24 is a full-rate VALU op;
@@ -127,9 +126,6 @@ struct Lane {
   uint32_t pops;  // packets this node delivered as a sender: tokens (lo16) | markers (hi16); <= 1 per tick
   uint32_t hw[2];   // (head words in registers, unrolled D <= 4) out-link k's head word: u16 k & 1 of word k >> 1
   uint32_t cur[2];  // (cursors in registers, unrolled D <= 4) in-link k's recording cursor: u16 k & 1 of word k >> 1
-  // (segment completion, Ctx::dpp_done, s_cap <= 16) lo16: the snapshots this node has
-  // completed (node.go:165); hi16: those its instance has completed (uniform over the segment)
-  uint32_t nd;
   bool alive;    // instance still running (uniform within the segment)
   int32_t flag;  // lane-local engine failure raised during an op/tick
 #if CLSNAP_PROF
@@ -168,18 +164,11 @@ using InLinks = uint32_t[unrolled(D) ? D : 1];
 #ifndef CLSNAP_CURREG
 #define CLSNAP_CURREG 1
 #endif
-// Out-link head words (8-bit ring head, 8-bit count) of the unrolled kernels in two packed
-// registers instead of the link words' lo16 halves (A/B knob): phase A's and the pushes' LDS
-// reads + writes become register ops; the halves are refreshed for the epilogue.
-#ifndef CLSNAP_HWREG
-#define CLSNAP_HWREG 0
-#endif
-// Snapshot completion (sim.go:126-131) detected once per tick by a segment-wide AND of the
-// nodes' completed-snapshot masks (DPP, aligned power-of-two segments of at most 16 lanes)
-// instead of an LDS atomic counter per (instance, snapshot) on every local completion; the
-// instance's completed mask stays in a register (A/B knob CLSNAP_DPPDONE, cl_engine.h
-// seg_done_mode).
-constexpr bool hw_reg(int D) { return CLSNAP_HWREG && D <= 4 && CLSNAP_UNROLL_MAX >= D; }
+// Out-link head words (8-bit ring head, 8-bit count) of the unrolled kernels live in two
+// packed registers instead of the link words' lo16 halves: phase A's and the pushes' LDS
+// reads + writes become register ops; the halves are refreshed for the epilogue (r04 A/B,
+// gpurun_out/r04a: C3 2.380 -> 2.353 ms per step, C2 0.180 -> 0.176 ms).
+constexpr bool hw_reg(int D) { return D <= 4 && CLSNAP_UNROLL_MAX >= D; }
 constexpr bool cur_reg(int D) { return CLSNAP_CURREG && D <= 4 && unrolled(D); }
 
 #define PW(k) (x.P[(uint32_t)(k) << 6])
@@ -326,10 +315,6 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
 // nodes have; one LDS counter per (instance, snapshot).
 // (u8 counters, four per word: a count never exceeds N <= 64, so the add never carries)
 __device__ __forceinline__ void node_complete(const Ctx& x, Lane& ln, int32_t sid) {
-  if (x.dpp_done) {  // counted once per tick by seg_complete
-    ln.nd |= 1u << sid;
-    return;
-  }
   const uint32_t sh = ((uint32_t)sid & 3u) * 8u;
   const uint32_t old = lds_add(&XW(x.lay.x_done + x.seg * x.lay.sp + (sid >> 2)), 1u << sh);
   if (((old >> sh) & 0xffu) + 1 == (uint32_t)x.p.n_nodes) {
@@ -405,32 +390,6 @@ __device__ __forceinline__ void refill(const Ctx& x, int32_t ko, uint32_t slot) 
   const uint32_t h = *hp;
   PW(slot) = x.p.ovf[((c << lay.ocap_log2) + h) * x.stride + x.inst];
   *hp = (h + 1) & om;
-}
-
-// AND of v over this lane's instance segment: aligned power-of-two segments of at most 16
-// lanes, DPP butterflies (every lane of the wave must be active).
-__device__ __forceinline__ uint32_t seg_and(int32_t N, uint32_t v) {
-  if (N >= 2) v &= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);   // quad_perm 1,0,3,2
-  if (N >= 4) v &= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);   // quad_perm 2,3,0,1
-  if (N >= 8) v &= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
-  if (N >= 16) v &= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false); // row_mirror
-  return v;
-}
-
-// NotifyCompletedSnapshot (sim.go:126-131) for the snapshots every node of the instance has
-// completed by now (Ctx::dpp_done): the segment's first lane stores their completion tick.
-// Must be reached by all lanes of the wave.
-__device__ __forceinline__ void seg_complete(const Ctx& x, Lane& ln) {
-  const uint32_t all = seg_and(x.p.n_nodes, ln.nd) & 0xffffu;
-  uint32_t nw = all & ~(ln.nd >> 16);
-  if (!nw) return;
-  ln.nd |= nw << 16;
-  if (x.v == 0)
-    while (nw) {
-      const uint32_t sid = (uint32_t)__builtin_ctz(nw);
-      nw &= nw - 1;
-      st_snap(x.p.snap_tick, 4u * (x.inst * (uint32_t)x.lay.s_cap + sid), ln.time);
-    }
 }
 
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
@@ -532,8 +491,6 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       handle_marker<D, TRACE>(x, ln, it, ki, w, src, (int32_t)pay, ntrig);
     }
   }
-  // (segment completion: once per tick, when some node completed a snapshot in it)
-  if (x.dpp_done && __ballot((ln.nd ^ (ln.nd >> 16)) & 0xffffu)) seg_complete(x, ln);
   // ---- C/D: broadcast draws in sender order, then push -------------------------
   const unsigned long long pt1 = PROF_T();
   PROF_ADD(ln, 2, pt0);
@@ -680,7 +637,7 @@ constexpr int waves_for(int D, bool spill) {
 
 // The whole event program for the instances of one wave (slots wave * ipw .. + ipw - 1 of
 // the launch; n_slots slots in all).  Every lane of the wave must call it.
-template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED, bool SEG>
+template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED>
 __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay, uint32_t wave, uint32_t n_slots,
                                           const int32_t* imap, lds_u32* X, const uint32_t* __restrict__ topo,
                                           const Op* __restrict__ ops, const uint8_t* __restrict__ sched) {
@@ -721,8 +678,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
               indeg, outdeg, valid ? (int32_t)nb[2] : 0,
               4u * st * (uint32_t)N * (uint32_t)lay.rw,
               (int32_t)(p.draws < 0x7fffffffLL ? p.draws : 0x7fffffffLL),
-              4ull * st * (uint64_t)N * (uint64_t)lay.rw < (1ull << 24),
-              SEG};
+              4ull * st * (uint64_t)N * (uint64_t)lay.rw < (1ull << 24)};
   InLinks<D> it;
   if constexpr (unrolled(D)) {
 #pragma unroll
@@ -750,7 +706,6 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
     ln.started = 0;
     ln.time = ln.draw = ln.status = 0;
     ln.peek = ln.pops = ln.push = 0;
-    ln.nd = 0;
   } else {
     const uint32_t* S = p.state + ii;
     const uint32_t b = (uint32_t)v * (lay.priv + G_NUM);
@@ -773,18 +728,6 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
         XW(lay.x_done + seg * lay.sp + q) = w;
       }
       XW(lay.x_ndone + seg) = Dn[lay.s_cap * st];
-    }
-    // (segment completion) the instance's completed snapshots from the saved counters; a
-    // node has completed snapshot s when it started it, its pending count is 0 and it has
-    // in-links (an initiator without in-links never completes, node.go:165)
-    ln.nd = 0;
-    if (x.dpp_done && valid) {
-      const uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
-      for (int32_t q = 0; q < lay.s_cap; ++q) {
-        ln.nd |= (int32_t)Dn[q * st] == N ? 1u << (16 + q) : 0u;
-        const uint32_t pend = (PW(lay.w_pend + (q >> 2)) >> ((q & 3) * 8)) & 0xffu;
-        ln.nd |= (((ln.started >> q) & 1u) && pend == 0 && indeg > 0) ? 1u << q : 0u;
-      }
     }
   }
   if constexpr (!unrolled(D))
@@ -848,8 +791,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
       int32_t rem = drain ? op.b : op.a;
       bool waiting = drain;
       for (int32_t iter = 0;; ++iter) {
-        if (waiting && (!ln.alive || (x.dpp_done ? __builtin_popcount(ln.nd >> 16) : (int32_t)XW(lay.x_ndone + seg)) >= n_started))
-          waiting = false;
+        if (waiting && (!ln.alive || (int32_t)XW(lay.x_ndone + seg) >= n_started)) waiting = false;
         if (waiting && iter >= op.a) {
           ln.status = ST_HANG;
           ln.alive = false;
@@ -920,7 +862,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
     r[R_TIME] = ln.time;
     r[R_DRAW] = ln.draw;
     r[R_STATUS] = ln.status;
-    r[R_NDONE] = x.dpp_done ? __builtin_popcount(ln.nd >> 16) : (int32_t)XW(lay.x_ndone + seg);
+    r[R_NDONE] = (int32_t)XW(lay.x_ndone + seg);
     r[R_PEEK] = (int32_t)acc[0];
     r[R_POP_TOK] = (int32_t)acc[1];
     r[R_POP_MK] = (int32_t)acc[2];
@@ -934,16 +876,6 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
       if (k < indeg) CUR(k) = (uint16_t)cur_get<D>(x, ln, k);
   }
   uint32_t* S = p.state + ii;
-  // (segment completion) the saved per-snapshot counters of completed nodes: a ballot per
-  // snapshot (every valid lane is still here)
-  if (x.dpp_done) {
-    const uint64_t segm = N == 64 ? ~0ull : (((1ull << N) - 1) << x.seg_base);
-    uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
-    for (int32_t q = 0; q < lay.s_cap; ++q) {
-      const uint32_t c = (uint32_t)__popcll(__ballot((ln.nd >> q) & 1u) & segm);
-      if (v == 0) Dn[q * st] = c;
-    }
-  }
   const uint32_t b = (uint32_t)v * (lay.priv + G_NUM);
   for (int32_t k = 0; k < lay.priv; ++k) S[(b + k) * st] = PW(k);
   uint32_t* R = S + (b + lay.priv) * st;
@@ -958,287 +890,8 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   R[G_PUSH * st] = ln.push;
   if (v == 0) {
     uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
-    if (!x.dpp_done)
-      for (int32_t s = 0; s < lay.s_cap; ++s) Dn[s * st] = (XW(lay.x_done + seg * lay.sp + (s >> 2)) >> ((s & 3) * 8)) & 0xffu;
-    Dn[lay.s_cap * st] = x.dpp_done ? (uint32_t)__builtin_popcount(ln.nd >> 16) : XW(lay.x_ndone + seg);
-  }
-}
-
-// ---- refill mode ----------------------------------------------------------------------
-// A full run that saves no state (cl_rerun: replays and first launches of a program) on a
-// persistent grid: each segment of a wave runs one instance after another, pulling work
-// items from shared counters, so a wave's segments never idle until the longest of a fixed
-// group of instances is done, and the grid has no tail of partly filled rounds (the 2^17
-// per-GPU share of an 8-GPU node is 2.7 rounds of waves).  Per segment, the position in the
-// event program (pc), the tick op's remaining ticks and the drain's waiting budget are lane
-// registers, uniform over the segment; the non-tick ops run for the segments that reached
-// them, one op index at a time.  Work item i (slot slot_base + i; instance imap[slot] when
-// mapped) belongs to counter i % kRefillShards, so every counter serves items in slot order
-// (a length-ordered map stays longest first).
-constexpr uint32_t kRefillShards = 8;
-constexpr uint32_t kRefillGrab = 8;  // items a wave takes per counter atomic
-
-// The outputs of the instances of finishing segments (`fin`): tokens still queued, the
-// per-instance sums (the exec epilogue), the final node tokens.  All lanes must call.
-template <int D>
-__device__ __forceinline__ void refill_outputs(const Ctx& x, Lane& ln, bool fin) {
-  const ExecParams& p = x.p;
-  const Layout& lay = x.lay;
-  if constexpr (hw_reg(D)) {  // the link words' head halves
-#pragma unroll
-    for (int32_t k = 0; k < D; ++k)
-      if (fin && k < lay.od) CHW(k) = (uint16_t)hw_get<D>(x, ln, k);
-  }
-  int32_t inflight = 0;
-  if (fin) {
-    const uint32_t cap = 1u << lay.cap_log2;
-    for (int32_t ko = 0; ko < x.outdeg; ++ko) {
-      const uint32_t chw = CHW(ko);
-      const uint32_t cnt = chw >> 8, head = chw & 0xffu;
-      for (uint32_t k = 0; k < cnt && k < cap; ++k) {
-        const uint32_t e = PW(lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + ((head + k) & (cap - 1)));
-        if (!(e & kMarkerBit)) inflight += (int32_t)(e & 0xffffu);
-      }
-      if (cnt > cap) {
-        const uint32_t c = (uint32_t)(x.out_off + ko);
-        const uint32_t om = (1u << lay.ocap_log2) - 1;
-        const uint32_t h = p.ovh[c * x.stride + x.inst];
-        for (uint32_t k = 0; k < cnt - cap; ++k) {
-          const uint32_t e = p.ovf[((c << lay.ocap_log2) + ((h + k) & om)) * x.stride + x.inst];
-          if (!(e & kMarkerBit)) inflight += (int32_t)(e & 0xffffu);
-        }
-      }
-    }
-    lds_u32* acc = &XW(lay.x_acc + 5 * x.seg);
-    lds_add(acc + 0, ln.peek);
-    lds_add(acc + 1, ln.pops & 0xffffu);
-    lds_add(acc + 2, ln.pops >> 16);
-    lds_add(acc + 3, ln.push);
-    lds_add(acc + 4, (uint32_t)inflight);
-  }
-  wave_sync();
-  if (fin) {
-    p.fin_tok[x.inst * (uint32_t)p.n_nodes + x.v] = ln.tokens;
-    if (x.v == 0) {
-      lds_u32* acc = &XW(lay.x_acc + 5 * x.seg);
-      int32_t* r = p.regs + (size_t)x.inst * R_NUM;
-      r[R_TIME] = ln.time;
-      r[R_DRAW] = ln.draw;
-      r[R_STATUS] = ln.status;
-      r[R_NDONE] = x.dpp_done ? __builtin_popcount(ln.nd >> 16) : (int32_t)XW(lay.x_ndone + x.seg);
-      r[R_PEEK] = (int32_t)acc[0];
-      r[R_POP_TOK] = (int32_t)acc[1];
-      r[R_POP_MK] = (int32_t)acc[2];
-      r[R_PUSH] = (int32_t)acc[3];
-      r[R_INFLIGHT_TOK] = (int32_t)acc[4];
-#pragma unroll
-      for (int q = 0; q < 5; ++q) acc[q] = 0u;  // (the segment's next instance)
-    }
-  }
-}
-
-// Refill mode: one segment's program state, uniform over its lanes, packed in two registers:
-// pc = next op (bits 15..0; op_end: done) | snapshots started before the drain (23..16) |
-// has an instance (24) | inside a tick op (25) | the drain is waiting (26); tc = the tick op's
-// ticks left (15..0; drain: the extra ticks after the wait) | the drain's waiting budget
-// (31..16).  (cl_host.cpp refill_program_ok keeps every field in range.)
-constexpr uint32_t kSrHas = 1u << 24, kSrTick = 1u << 25, kSrWait = 1u << 26;
-
-template <int D, bool STAGED, int CAP, bool SPILL, bool SEG>
-__device__ __forceinline__ void exec_refill(const ExecParams& p, const Layout& lay, uint32_t wave, lds_u32* X,
-                                            const uint32_t* __restrict__ topo, const Op* __restrict__ ops,
-                                            const uint8_t* __restrict__ sched) {
-  constexpr bool TRACE = false;
-  const int32_t N = p.n_nodes;
-  const int32_t lane = threadIdx.x & (kWave - 1);
-  const int32_t seg = lane / N;
-  const int32_t v = lane - seg * N;
-  const bool segok = seg < lay.ipw;  // lanes past the wave's last full segment run nothing
-  const uint32_t* nb = topo + (size_t)(segok ? v : 0) * p.topo_w;
-  const int32_t indeg = segok ? (int32_t)nb[0] : 0;
-  const int32_t outdeg = segok ? (int32_t)nb[1] : 0;
-  const uint32_t st = (uint32_t)p.stride;
-  const uint32_t rw4 = (uint32_t)(p.sched_row / 4);
-  const lds_u8* lrow = (const lds_u8*)(X + lay.x_delay) + (size_t)seg * p.sched_row;
-  Ctx x{p, lay, X + lay.col + lane, X, sched, lrow, lane, seg * N, v, seg, 0u, st,
-        indeg, outdeg, segok ? (int32_t)nb[2] : 0,
-        4u * st * (uint32_t)N * (uint32_t)lay.rw,
-        (int32_t)(p.draws < 0x7fffffffLL ? p.draws : 0x7fffffffLL),
-        4ull * st * (uint64_t)N * (uint64_t)lay.rw < (1ull << 24),
-        SEG};
-  InLinks<D> it;
-#pragma unroll
-  for (int32_t k = 0; k < D; ++k) it[k] = k < indeg ? nb[3 + k] : 0u;
-  for (int32_t k = lane; k < lay.x_delay_begin; k += kWave) XW(k) = 0u;
-  Lane ln;
-  ln.flag = 0;
-  ln.alive = false;
-  ln.tokens = 0;
-  ln.started = 0;
-  ln.time = ln.draw = ln.status = 0;
-  ln.peek = ln.pops = ln.push = 0;
-  ln.cur[0] = ln.cur[1] = 0;
-  ln.hw[0] = ln.hw[1] = 0;
-  ln.nd = 0;
-  uint32_t pc = 0, tc = 0;
-  // the wave's work queue, in its LDS words (rarely touched): items shard + kRefillShards *
-  // [qn, qe) of counter `shard`; q2 = shard | counters tried << 8 | exhausted << 16
-  if (lane == 0) {
-    XW(lay.x_q + 0) = 0u;
-    XW(lay.x_q + 1) = 0u;
-    XW(lay.x_q + 2) = wave % kRefillShards;
-  }
-  const uint32_t n_items = (uint32_t)p.n_inst - p.slot_base;
-  wave_sync();
-
-  for (;;) {
-    // ---- settle: every segment with an instance sits in a tick op that ticks now ------
-    for (;;) {
-      // (a) finished instances: outputs; then the next work item for every free segment
-      const bool fin = (pc & kSrHas) && (pc & 0xffffu) >= (uint32_t)p.op_end;
-      if (__ballot(fin)) {
-        refill_outputs<D>(x, ln, fin);
-        if (fin) {
-          pc = 0;
-          ln.nd = 0;  // (an idle segment must not look like a pending completion)
-        }
-      }
-      uint64_t want = __ballot(segok && !(pc & kSrHas) && v == 0);
-      uint32_t q2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)XW(lay.x_q + 2));
-      bool got = false;
-      uint32_t item = 0;
-      if (want && !(q2 & 0x10000u)) {
-        uint32_t qn = (uint32_t)__builtin_amdgcn_readfirstlane((int)XW(lay.x_q + 0));
-        uint32_t qe = (uint32_t)__builtin_amdgcn_readfirstlane((int)XW(lay.x_q + 1));
-        while (want) {
-          const int32_t l = (int32_t)__builtin_ctzll(want);
-          want &= want - 1;
-          if (qn == qe) {  // the next kRefillGrab items of a counter (one atomic per wave)
-            bool ok = false;
-            while ((q2 >> 8 & 0xffu) < kRefillShards) {
-              const uint32_t sh = q2 & 0xffu;
-              uint32_t g = 0;
-              if (lane == 0) g = atomicAdd(&p.work[sh], kRefillGrab);
-              g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
-              const uint32_t cnt = n_items > sh ? (n_items - sh + kRefillShards - 1) / kRefillShards : 0u;
-              if (g < cnt) {
-                qn = g;
-                qe = min(g + kRefillGrab, cnt);
-                ok = true;
-                break;
-              }
-              q2 = ((sh + 1) % kRefillShards) | (((q2 >> 8 & 0xffu) + 1) << 8);
-            }
-            if (!ok) {
-              q2 |= 0x10000u;
-              break;
-            }
-          }
-          const uint32_t i = (q2 & 0xffu) + kRefillShards * qn++;
-          if (seg == l / N) {
-            got = true;
-            item = i;
-          }
-        }
-        if (lane == 0) {
-          XW(lay.x_q + 0) = qn;
-          XW(lay.x_q + 1) = qe;
-          XW(lay.x_q + 2) = q2;
-        }
-      }
-      if (__ballot(got)) {
-        // a new instance for the segments that got an item: fresh state (the exec prologue)
-        if (got) {
-          const uint32_t slot = p.slot_base + item;
-          x.inst = p.inst_map ? (uint32_t)p.inst_map[slot] : slot;
-          for (int32_t sid = v; sid < lay.s_cap; sid += N)
-            st_at(p.snap_tick, 4u * (x.inst * (uint32_t)lay.s_cap + (uint32_t)sid), (int32_t)-1);
-          const uint32_t* src = reinterpret_cast<const uint32_t*>(sched + (size_t)x.inst * p.sched_row);
-          for (uint32_t k = (uint32_t)v; k < rw4; k += (uint32_t)N) X[lay.x_delay + (uint32_t)seg * rw4 + k] = src[k];
-          for (int32_t k = 0; k < lay.priv; ++k) PW(k) = 0u;
-          if (!SEG && v == 0) {
-            for (int32_t q = 0; q < lay.sp; ++q) XW(lay.x_done + seg * lay.sp + q) = 0u;
-            XW(lay.x_ndone + seg) = 0u;
-          }
-          ln.tokens = (int32_t)topo[(size_t)N * p.topo_w + v];
-          ln.started = 0;
-          ln.time = ln.draw = ln.status = 0;
-          ln.peek = ln.pops = ln.push = 0;
-          ln.cur[0] = ln.cur[1] = 0;
-          ln.hw[0] = ln.hw[1] = 0;
-          ln.nd = 0;
-          ln.alive = true;
-          pc = kSrHas | (uint32_t)p.op_begin;
-          tc = 0;
-        }
-        wave_sync();
-      }
-      // (b) the non-tick ops of segments between ticks, one op index at a time (a frozen
-      // instance skips the rest of its program: nothing in it would run)
-      for (;;) {
-        if ((pc & kSrHas) && !(pc & kSrTick) && !ln.alive) pc = (pc & ~0xffffu) | (uint32_t)p.op_end;
-        const bool need = (pc & kSrHas) && !(pc & kSrTick) && (pc & 0xffffu) < (uint32_t)p.op_end;
-        const uint64_t m = __ballot(need);
-        if (!m) break;
-        const int32_t sel = __builtin_amdgcn_readlane((int)(pc & 0xffffu), (int32_t)__builtin_ctzll(m));
-        const Op op = ops[sel];
-        const bool mine = need && (int32_t)(pc & 0xffffu) == sel;
-        if (op.kind == OP_TICK || op.kind == OP_DRAIN) {
-          if (mine) {
-            const bool dr = op.kind == OP_DRAIN;
-            pc = (pc & (0xffffu | kSrHas)) | kSrTick | (dr ? kSrWait | ((uint32_t)op.c << 16) : 0u);
-            tc = (uint32_t)(dr ? op.b : op.a) | ((uint32_t)op.a << 16);
-          }
-          continue;
-        }
-        const bool keep = ln.alive && !mine;  // other segments' instances sit this op out
-        ln.alive = ln.alive && mine;
-        int32_t adv = 1;
-        if (op.kind == OP_SEND) {
-          send_one<D, STAGED, TRACE>(x, ln, op, sel);
-        } else if (op.kind == OP_SENDS) {
-          send_group<D, STAGED, TRACE>(x, ln, ops + sel + 1, op.a, sel + 1);
-          adv = 1 + op.a;
-        } else {  // OP_SNAP: sim.StartSnapshot -> node.StartSnapshot (see exec_wave)
-          if (ln.alive && v == op.a) {
-            ln.started |= 1u << op.b;
-            create_local<D>(x, ln, it, op.b, -1);
-            const uint32_t pi = lay.w_pend + (op.b >> 2), sh = (op.b & 3) * 8;
-            PW(pi) = (PW(pi) & ~(0xffu << sh)) | ((uint32_t)indeg << sh);
-#pragma unroll
-            for (int32_t j = 0; j < D; ++j)
-              if (j < outdeg) push<D, STAGED>(x, ln, j, kMarkerBit | (uint32_t)op.b, ln.draw + j);
-          }
-          if (ln.alive) ln.draw += op.c;
-          resolve_failures(x, ln);
-        }
-        if (mine) pc += (uint32_t)adv;
-        ln.alive = ln.alive || keep;
-      }
-      // (c) the tick op's checks before each tick (test_common.go:123-137, see exec_wave)
-      bool ended = false;
-      if ((pc & kSrHas) && (pc & kSrTick)) {
-        if (pc & kSrWait) {
-          const int32_t nd = x.dpp_done ? __builtin_popcount(ln.nd >> 16) : (int32_t)XW(lay.x_ndone + seg);
-          if (!ln.alive || nd >= (int32_t)((pc >> 16) & 0xffu)) {
-            pc &= ~kSrWait;
-          } else if ((tc >> 16) == 0) {
-            ln.status = ST_HANG;
-            ln.alive = false;
-            pc &= ~kSrWait;
-          }
-        }
-        if (!(ln.alive && ((pc & kSrWait) || (tc & 0xffffu) > 0))) {
-          pc = (pc & (0xffffu | kSrHas)) + 1u;  // (clears the tick-op bits)
-          ended = true;
-        }
-      }
-      if (!__ballot(ended)) break;
-    }
-    if (!__ballot(pc & kSrHas)) break;
-    const bool act = (pc & kSrHas) && (pc & kSrTick);  // (settled: every such instance ticks now)
-    tick<D, STAGED, TRACE>(x, ln, it, act);
-    if (act) tc -= (pc & kSrWait) ? 0x10000u : 1u;
+    for (int32_t s = 0; s < lay.s_cap; ++s) Dn[s * st] = (XW(lay.x_done + seg * lay.sp + (s >> 2)) >> ((s & 3) * 8)) & 0xffu;
+    Dn[lay.s_cap * st] = XW(lay.x_ndone + seg);
   }
 }
 
@@ -1246,7 +899,7 @@ __device__ __forceinline__ void exec_refill(const ExecParams& p, const Layout& l
 // pressure of the D = 3 kernel 95 VGPRs + 58 SGPR spills -> ~80 VGPRs, no spills); SPILL false
 // compiles out the HBM spill rings.  CAP = 0 reads every offset from the runtime layout (any
 // D, any ring size).  The grid covers slots [p.slot_base, p.n_inst).
-template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED, bool SEG, bool REFILL>
+template <int D, bool STAGED, bool TRACE, int CAP, bool SPILL, bool MAPPED>
 __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D, SPILL)) void cl_exec_kernel(
     ExecParams p, const uint32_t* __restrict__ topo, const Op* __restrict__ ops, const uint8_t* __restrict__ sched) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1269,12 +922,8 @@ __global__ __launch_bounds__(kWave * kWavesPerBlock, waves_for(D, SPILL)) void c
   const Layout& lay = lay_;
   const int32_t wib = threadIdx.x / kWave;
   lds_u32* X = (lds_u32*)(lds + (size_t)wib * lay.wave_words);
-  if constexpr (REFILL)
-    exec_refill<D, STAGED, CAP, SPILL, SEG>(p, lay, blockIdx.x * (uint32_t)p.lay.wpb + wib, X, topo, ops, sched);
-  else
-    exec_wave<D, STAGED, TRACE, CAP, SPILL, MAPPED, SEG>(p, lay, blockIdx.x * (uint32_t)p.lay.wpb + wib,
-                                                         (uint32_t)p.n_inst, MAPPED ? p.inst_map : nullptr, X, topo,
-                                                         ops, sched);
+  exec_wave<D, STAGED, TRACE, CAP, SPILL, MAPPED>(p, lay, blockIdx.x * (uint32_t)p.lay.wpb + wib, (uint32_t)p.n_inst,
+                                                  MAPPED ? p.inst_map : nullptr, X, topo, ops, sched);
 }
 
 #undef PW
@@ -1465,29 +1114,18 @@ __global__ __launch_bounds__(256) void cl_pack_fill(PackParams p) {
 }  // namespace
 
 // `stream`: launch there instead of L.stream, without the timing events unless `events`.
-template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true, bool SEG = false,
-          bool REFILL = false>
+template <int D, bool STAGED, bool TRACE, int CAP = 0, bool SPILL = true, bool MAPPED = true>
 int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L,
                    void* stream = nullptr, bool events = false) {
   const int32_t wpb = p.lay.wpb;
   const size_t lds = (size_t)p.lay.wave_words * wpb * sizeof(uint32_t);
-  auto* k = cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED, SEG, REFILL>;
+  auto* k = cl_exec_kernel<D, STAGED, TRACE, CAP, SPILL, MAPPED>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLdsBytes);
     if (e != hipSuccess) return (int)e;
   }
   const int64_t waves = (p.n_inst - p.slot_base + p.lay.ipw - 1) / p.lay.ipw;
-  unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
-  if constexpr (REFILL) {
-    // persistent grid: the workgroups that are resident at once (more would only queue)
-    int per_cu = 0, dev = 0, cus = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, kWave * wpb, lds);
-    if (e != hipSuccess) return (int)e;
-    const int64_t resident = (int64_t)(per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1);
-    if ((int64_t)blocks > resident) blocks = (unsigned)resident;
-  }
+  const unsigned blocks = (unsigned)((waves + wpb - 1) / wpb);
   if (blocks == 0) return 0;
   const bool ev = !stream || events;
   hipExtLaunchKernelGGL(k, dim3(blocks), dim3(kWave * wpb), lds, (hipStream_t)(stream ? stream : L.stream),
@@ -1501,7 +1139,7 @@ int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, con
 // kernel (6 waves per SIMD for D = 3, 4), slots [split, n) on the spill-capable one,
 // concurrently on a second stream (fork / join events).  The main dispatch records the start
 // event; the stop event is recorded after the join.
-template <int D, int CAP, bool SEG>
+template <int D, int CAP>
 int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched,
                       const ExecLaunch& L) {
   hipStream_t s = (hipStream_t)L.stream, s2 = (hipStream_t)L.stream2;
@@ -1519,22 +1157,17 @@ int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, 
   ExecLaunch lb = L;
   lb.ev_stop = L.ev_stop2;
   int e;
-  // the spill-free part: a persistent refill grid when the launch allows it (p.refill)
-  auto main_part = [&](const ExecLaunch& l) {
-    return p.refill ? launch_exec_ds<D, true, false, CAP, false, true, SEG, true>(a, topo, ops, sched, l)
-                    : launch_exec_ds<D, true, false, CAP, false, true, SEG>(a, topo, ops, sched, l);
-  };
   if (CLSNAP_SPILL_FIRST) {
     // the spilling instances are the longest: their kernel is dispatched first so its
     // workgroups are resident from the start instead of queueing behind the main grid (the
     // tail of a small per-GPU batch); it records the start event
-    if ((e = launch_exec_ds<D, true, false, CAP, true, true, SEG>(b, topo, ops, sched, lb, s2, true))) return e;
+    if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
     la.ev_start = nullptr;
-    if ((e = main_part(la))) return e;
+    if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
   } else {
-    if ((e = main_part(la))) return e;
+    if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
     lb.ev_start = nullptr;
-    if ((e = launch_exec_ds<D, true, false, CAP, true, true, SEG>(b, topo, ops, sched, lb, s2, true))) return e;
+    if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
   }
   if (L.stop2_used && L.ev_stop2) *L.stop2_used = 1;
   if (!L.join) {  // replays back to back: the main stream does not wait for stream2 (cl_host.cpp)
@@ -1561,24 +1194,13 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
       const bool rings = p.lay.ocap_log2 >= 0 && !p.nospill;
       const bool mp = p.inst_map != nullptr;
       const bool split = CLSNAP_SPLIT && rings && mp && p.split_slot > 0 && p.split_slot < p.n_inst && L.stream2;
-      // instance completion by segment AND: aligned power-of-two instances of at most 16
-      // nodes and at most 16 snapshot ids (CLSNAP_DPPDONE)
-      const bool seg = seg_done_mode(p.n_nodes, p.lay.s_cap);
-#define CLSNAP_SPEC2(C, S)                                                                                    \
-  if (split) return launch_exec_split<D, C, S>(p, topo, ops, sched, L);                                     \
-  if (p.refill) return rings ? launch_exec_ds<D, true, false, C, true, true, S, true>(p, topo, ops, sched, L) \
-                             : launch_exec_ds<D, true, false, C, false, true, S, true>(p, topo, ops, sched, L); \
-  if (rings) return mp ? launch_exec_ds<D, true, false, C, true, true, S>(p, topo, ops, sched, L)           \
-                       : launch_exec_ds<D, true, false, C, true, false, S>(p, topo, ops, sched, L);         \
-  return mp ? launch_exec_ds<D, true, false, C, false, true, S>(p, topo, ops, sched, L)                     \
-            : launch_exec_ds<D, true, false, C, false, false, S>(p, topo, ops, sched, L);
-#define CLSNAP_SPEC(C)          \
-  case C:                       \
-    if (seg) {                  \
-      CLSNAP_SPEC2(C, true)     \
-    } else {                    \
-      CLSNAP_SPEC2(C, false)    \
-    }
+#define CLSNAP_SPEC(C)                                                                              \
+  case C:                                                                                           \
+    if (split) return launch_exec_split<D, C>(p, topo, ops, sched, L);                          \
+    if (rings) return mp ? launch_exec_ds<D, true, false, C, true, true>(p, topo, ops, sched, L)   \
+                         : launch_exec_ds<D, true, false, C, true, false>(p, topo, ops, sched, L); \
+    return mp ? launch_exec_ds<D, true, false, C, false, true>(p, topo, ops, sched, L)          \
+              : launch_exec_ds<D, true, false, C, false, false>(p, topo, ops, sched, L);
       switch (p.lay.cap_log2) {
         CLSNAP_SPEC(1)
         CLSNAP_SPEC(2)
@@ -1586,7 +1208,6 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
         default: break;
       }
 #undef CLSNAP_SPEC
-#undef CLSNAP_SPEC2
     }
   }
   return p.lay.x_delay > 0 ? launch_exec_ds<D, true, false>(p, topo, ops, sched, L)
