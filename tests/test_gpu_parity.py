@@ -369,6 +369,35 @@ def test_headline_batch_2p20_matches_fixture():
         sim.synchronize()
 
 
+def test_headline_batch_fresh_path_matches_fixture():
+    """The fresh path on the north_star batch: the FIRST launch of a new sim is
+    a rerun with no replay plan -- the whole batch on the spill-free kernel, then the
+    instances that overflowed their LDS rings again on the spill-capable kernel -- and its
+    batch checksums equal the oracle's over every instance (tests/golden/bench_sums.json).
+    The replays after it (through the plan that first run built) agree too."""
+    import json
+    fx = json.load(open(os.path.join(os.path.dirname(TEST_DATA), "bench_sums.json")))
+    want = fx["batches"]["c3"]["sums"]
+    n = fx["batches"]["c3"]["instances"]
+    sim = cl.ChandyLamportSim(n, seed_base=O.REFERENCE_SEED)
+    sim.read_topology_file(os.path.join(TEST_DATA, "8nodes.top"))
+    sim.read_events_file(os.path.join(TEST_DATA, "8nodes-concurrent-snapshots.events"))
+    sim.rerun()                    # the first launch: nothing derived from a prior run
+    sim.synchronize()
+    reruns = sim.fresh_reruns()
+    spilled, _ = sim.replay_split()
+    assert reruns > 0 and reruns == spilled, (reruns, spilled)  # the re-run set is the plan's spill set
+    for rnd in range(2):
+        got = dict(zip(cl.SUM_NAMES, sim.checksums().tolist()))
+        got["recorded"] = sim.counters(only_ok=True)["recorded"]
+        for k in want:
+            assert (got[k] - want[k]) % (1 << 64) == 0, f"pass {rnd} {k}: engine {got[k]} vs oracle {want[k]}"
+        sim.poison_outputs()
+        sim.rerun()                # a replay through the plan
+        sim.synchronize()
+        assert sim.fresh_reruns() == -1
+
+
 def test_two_event_texts_and_snapshot_after_drain():
     """Two readEventsFile calls on one batch, then a snapshot after the last drain and
     more ticks: every instance equals the oracle running the same calls; a rerun
