@@ -307,7 +307,6 @@ def main(argv=None):
     if fresh:
         fsum = cldist.reduce_results(0.0, [fresh["delivered"]], coll_dev)[1][0]
         fresh = {"fresh_run_ms": kmax[1], "packets_per_s": fsum / (kmax[1] * 1e-3), "packets": fsum,
-                 "reruns": fresh["reruns"],
                  "seeds": f"rand.Seed(REFERENCE_SEED + {total} + i): a batch of the same size the "
                           f"engine never ran", "note": fresh["note"]}
 
@@ -424,11 +423,11 @@ def fresh_run(cl, n, device, seed_base, top, events, args):
     f.synchronize()
     ms, launches = f.kernel_time()
     sums = dict(zip(cl.SUM_NAMES, f.checksums().tolist()))
-    return {"kernel_ms": ms / max(launches, 1), "delivered": sums["delivered"], "reruns": f.fresh_reruns(),
-            "note": "first launch of a new sim on unseen seeds (HIP events from the first pass's start to the "
-                    "last pass's end): the whole batch on the spill-free kernel, then the instances that "
-                    "overflowed their LDS rings again on the spill-capable kernel (reruns); not parity-pinned "
-                    "by a fixture -- the same fresh path on the fixture seeds is (tests/test_gpu_parity.py)"}
+    return {"kernel_ms": ms / max(launches, 1), "delivered": sums["delivered"],
+            "note": "first launch of a new sim on unseen seeds (HIP events): no replay plan, so the whole "
+                    "batch runs unordered on the spill-capable kernel; the same fresh path on the fixture "
+                    "seeds is parity-pinned (tests/test_gpu_parity.py test_headline_batch_fresh_path_matches_"
+                    "fixture)"}
 
 
 def b_alg_graph(c, n_nodes):

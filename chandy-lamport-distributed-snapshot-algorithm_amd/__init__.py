@@ -86,7 +86,6 @@ def lib():
         "cl_replay_mapped": [vp, vp],
         "cl_debug_poison_outputs": [vp],
         "cl_replay_split": [vp, vp, vp],
-        "cl_fresh_reruns": [vp, vp],
         "cl_num_nodes": [vp, vp],
         "cl_node_id": [vp, i32, vp],
         "cl_num_channels": [vp, vp],
@@ -421,13 +420,6 @@ class ChandyLamportSim:
         a, b = C.c_int64(0), C.c_int64(0)
         _check(self._L.cl_replay_split(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
-
-    def fresh_reruns(self):
-        """Instances the latest first full run re-ran on the spill-capable kernel after its
-        spill-free pass (-1: the latest launch was not such a run) -- cl_fresh_reruns."""
-        v = C.c_int64(0)
-        _check(self._L.cl_fresh_reruns(self._h, C.byref(v)))
-        return v.value
 
     def spill_free_replays(self):
         """True when the next rerun() runs wholly on the spill-free kernel (cl_replay_spill_free)."""

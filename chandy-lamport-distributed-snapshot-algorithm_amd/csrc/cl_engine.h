@@ -295,9 +295,6 @@ struct ExecLaunch {
 };
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
 int launch_checksums(const SumParams& p, void* stream);
-// Fresh runs (cl_host.cpp launch, CLSNAP_FRESH_FIXUP): the instances whose spill-free first
-// pass stopped with FIFO_OVERFLOW, compacted into list[0, *count).
-int launch_overflow_list(const int32_t* regs, int64_t n, int32_t* list, uint32_t* count, void* stream);
 
 // CollectSnapshot (sim.go:134-173) of snapshot `sid` for instances [lo, lo + n), packed on
 // the device (cl_kernels.hip): the node records' token words and the recording cursors are

@@ -55,12 +55,7 @@ constexpr int32_t kTargetBlocks = 6;
 // Batches of at least this many instances replay through a length-ordered slot map (a few
 // thousand waves: the grouping pays for its one host sort and 4 B per instance of HBM).
 constexpr int64_t kMapMinInstances = 4096;
-#ifndef CLSNAP_FRESH_FIXUP
-// A fresh full run (no plan yet) of a layout with spill rings: the whole batch on the
-// spill-free kernel, then the instances that overflowed their LDS rings again, compacted, on
-// the spill-capable one (A/B knob; 0: the whole batch on the spill-capable kernel).
-#define CLSNAP_FRESH_FIXUP 1
-#endif
+
 #ifndef CLSNAP_PIPE
 #define CLSNAP_PIPE 2  // split replays back to back: 0 join every replay, 1 neither fork nor join, 2 fork only (A/B knob)
 #endif
@@ -347,9 +342,6 @@ struct cl_sim {
   // wave end their drains together; replays of the same program and delays launch through
   // the map (results are per instance, unchanged).  -1: no map.
   DevBuf<int32_t> d_map;
-  DevBuf<int32_t> d_fix;     // fresh runs: instances whose spill-free pass overflowed
-  DevBuf<uint32_t> d_fixn;   // and their count
-  int64_t last_fixups = -1;  // the latest fresh run's re-run instances (-1: none)
   DevBuf<int32_t> d_hist;
   DevBuf<unsigned long long> d_sums;
   // device event trace (cl_trace_enable): instances [trace_lo, trace_lo + trace_n)
@@ -379,7 +371,7 @@ struct cl_sim {
       (void)hipStreamSynchronize(stream);
       d_ops.release(); d_topo.release(); d_sched.release(); d_state.release(); d_regs.release();
       d_snap_nod.release(); d_ch_slot.release(); d_snap_tick.release(); d_ovf.release(); d_fin_tok.release();
-      d_ovh.release(); d_spill_inst.release(); d_map.release(); d_fix.release(); d_fixn.release(); d_hist.release(); d_sums.release();
+      d_ovh.release(); d_spill_inst.release(); d_map.release(); d_hist.release(); d_sums.release();
       d_trace.release(); d_trace_cnt.release(); d_ch_dest.release();
       d_pk_tok.release(); d_pk_done.release(); d_pk_msg.release(); d_pk_cnt.release(); d_pk_bsum.release();
       d_pk_off.release(); d_rec2.release();
@@ -753,36 +745,10 @@ struct cl_sim {
     // step) and bracketed ~1 us of packet processing into the kernel time
     const bool pipe = CLSNAP_PIPE && planned && p.split_slot > 0 && p.split_slot < n_inst && stream2 && !save_state;
     if (!pipe && (rc = join_stream2())) return rc;
-    // fresh run with spill rings: spill-free first pass, then the overflowed instances again
-    const bool fixup = CLSNAP_FRESH_FIXUP && begin == 0 && !planned && trace_n == 0 && !save_state &&
-                       lay.ocap_log2 >= 0 && specialized();
-    ExecParams p1 = p;
-    if (fixup) p1.nospill = 1;
-    int e = launch_exec(p1, d_topo.p, d_ops.p, d_sched.p,
+    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p,
                         ExecLaunch{stream, pr.start, pr.stop, stream2, ev_fork, ev_join,
                                    pipe && CLSNAP_PIPE == 1 ? (s_dirty ? 1 : 0) : 1, pipe ? 0 : 1, pr.stop2,
                                    &pr.stop2_used});
-    last_fixups = -1;
-    if (e == 0 && fixup) {
-      if ((rc = d_fix.ensure((size_t)n_inst)) || (rc = d_fixn.ensure(1))) return rc;
-      e = launch_overflow_list(d_regs.p, n_inst, d_fix.p, d_fixn.p, stream);
-      uint32_t nfix = 0;
-      if (e == 0) {
-        HIP_TRY(hipMemcpyAsync(&nfix, d_fixn.p, sizeof nfix, hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
-        last_fixups = nfix;
-      }
-      if (e == 0 && nfix > 0) {
-        // the re-run on the spill-capable kernel through the compacted list; its dispatch
-        // records the launch's second stop event, so the launch time spans both passes
-        ExecParams p2 = p;
-        p2.inst_map = d_fix.p;
-        p2.n_inst = nfix;
-        e = launch_exec(p2, d_topo.p, d_ops.p, d_sched.p,
-                        ExecLaunch{stream, nullptr, pr.stop2, stream2, ev_fork, ev_join, 1, 1, nullptr, nullptr});
-        if (e == 0) pr.stop2_used = 1;
-      }
-    }
     if (pipe) {
       s2_live = true;
       s_dirty = false;
@@ -1326,13 +1292,6 @@ int cl_replay_spill_free(cl_sim* sim, int32_t* on) {
   int rc = sim->sync();
   if (rc) return rc;
   *on = sim->lay.ocap_log2 < 0 || (sim->plan_ops == (int64_t)sim->ops.size() && sim->plan_nospill) ? 1 : 0;
-  return CL_OK;
-}
-
-int cl_fresh_reruns(cl_sim* sim, int64_t* instances) {
-  SIM_CHECK(sim);
-  if (!instances) return set_err(CL_E_INVALID, "null output");
-  *instances = sim->last_fixups;
   return CL_OK;
 }
 

@@ -1261,30 +1261,6 @@ extern "C" int cl_prof_read(unsigned long long* out, int reset) {
 }
 #endif
 
-// The instances of [0, n) that stopped with FIFO_OVERFLOW (the spill-free first pass of a
-// fresh run): their indices, in any order, and how many.
-__global__ __launch_bounds__(256) void cl_overflow_list(const int32_t* __restrict__ regs, int64_t n,
-                                                         int32_t* __restrict__ list, uint32_t* __restrict__ count) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool ov = i < n && regs[i * R_NUM + R_STATUS] == ST_FIFO_OVERFLOW;
-  // one atomic per wave: the wave's overflowed instances take consecutive entries
-  const uint64_t m = __ballot(ov);
-  if (!m) return;
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t base = 0;
-  if (lane == (uint32_t)__builtin_ctzll(m)) base = atomicAdd(count, (uint32_t)__popcll(m));
-  base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(m));
-  if (ov) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (int32_t)i;
-}
-
-int launch_overflow_list(const int32_t* regs, int64_t n, int32_t* list, uint32_t* count, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(count, 0, sizeof(uint32_t), s);
-  if (e != hipSuccess) return (int)e;
-  if (n > 0) hipLaunchKernelGGL(cl_overflow_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, regs, n, list, count);
-  return (int)hipGetLastError();
-}
-
 int launch_checksums(const SumParams& p, void* stream) {
   const unsigned blocks = (unsigned)((p.n_inst + 255) / 256);
   hipLaunchKernelGGL(cl_checksum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p);

@@ -156,11 +156,6 @@ int cl_replay_spill_free(cl_sim* sim, int32_t* on);
  * spill-capable kernel while the slots before it run spill-free, concurrently (0: no split).
  * Engine-internal; results are the same either way. */
 int cl_replay_split(cl_sim* sim, int64_t* spill_instances, int64_t* split_slot);
-/* The latest first full run of a program that saved no state (no replay plan yet) ran the
- * whole batch on the spill-free kernel and re-ran, on the spill-capable kernel, the
- * instances whose queues outgrew the LDS rings: how many (-1: the latest launch was not such
- * a run).  Engine-internal; results are the same either way. */
-int cl_fresh_reruns(cl_sim* sim, int64_t* instances);
 /* 1 in *on when the next cl_rerun launches through the replay plan's slot map (instances
  * grouped by the final tick of an earlier full run of the same program and delays, so the
  * instances sharing a wave finish together, and those that spilled last; engine-internal,
