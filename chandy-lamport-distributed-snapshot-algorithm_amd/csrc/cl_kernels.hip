@@ -69,15 +69,17 @@ struct Ctx {
   int32_t indeg, outdeg, out_off;
   // snapshot outputs by 32-bit byte offsets from the (uniform) array bases: the stores use
   // the SGPR-base + 32-bit-VGPR-offset form, with no 64-bit address arithmetic per store
-  uint32_t nod_plane;  // bytes per sid plane of the node records (uniform)
+  uint32_t nod_plane8;  // bytes per sid plane of the node records / 256 (uniform; stride % 64 == 0)
   int32_t draws;       // delays per instance, clamped to int32 (draw indices are int32)
-  bool mul24;  // every plane offset sid * plane fits the 24-bit multiplier
 };
 
-// Byte offset of snapshot plane `sid` (sid < 32).  v_mul_u32_u24 is a full-rate VALU op;
-// a generic 32-bit multiply is quarter rate, a 64-bit index computation several ops.
-__device__ __forceinline__ uint32_t plane_off(const Ctx& x, uint32_t sid, uint32_t plane) {
-  return x.mul24 ? __umul24(sid, plane) : sid * plane;
+// Byte offset of snapshot plane `sid` (sid < 32): the plane is a multiple of 256 bytes (the
+// instance stride is a multiple of 64), so sid * (plane / 256) fits the full-rate 24-bit
+// multiplier (a generic 32-bit multiply is quarter rate) and the shift restores it.
+__device__ __forceinline__ uint32_t plane_off(const Ctx& x, uint32_t sid, uint32_t plane8) {
+  uint32_t m = __umul24(sid, plane8);
+  asm volatile("" : "+v"(m));  // (else the compiler re-forms sid * plane: a quarter-rate multiply)
+  return m << 8;
 }
 // This lane's byte offsets in snapshot plane 0, recomputed at each store (cheaper than
 // keeping them live in VGPRs through the tick loop).
@@ -283,7 +285,7 @@ __device__ __forceinline__ void create_local(const Ctx& x, Lane& ln, const InLin
                                              int32_t arrive) {
   const ExecParams& p = x.p;
   const Layout& lay = x.lay;
-  const uint32_t rb = plane_off(x, (uint32_t)sid, x.nod_plane) + nod_lane(x);
+  const uint32_t rb = plane_off(x, (uint32_t)sid, x.nod_plane8) + nod_lane(x);
   if constexpr (unrolled(D)) {
     // the whole record in one vector store (RW words: a power of two, Layout::rw)
     constexpr int RW = D == 1 ? 2 : D <= 3 ? 4 : 8;
@@ -367,10 +369,13 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
       ntrig++;
     }
   } else {  // later marker: stop recording this channel
-    // hi16 of the cursor word: the channel's end
-    st_snap(reinterpret_cast<uint16_t*>(x.p.snap_nod),
-          plane_off(x, (uint32_t)sid, x.nod_plane) + nod_lane(x) + 4u * (1 + (uint32_t)ki) + 2u,
-          (uint16_t)cur_get<D>(x, ln, ki));
+    // hi16 of the cursor word: the channel's end.  The record's offset is pinned in one
+    // VGPR (empty asm) so the in-link's constant folds into the store's immediate offset
+    // instead of the compiler keeping a 64-bit base per in-link live through the tick loop.
+    uint32_t rb = plane_off(x, (uint32_t)sid, x.nod_plane8) + nod_lane(x);
+    asm volatile("" : "+v"(rb));
+    st_snap(reinterpret_cast<uint16_t*>(x.p.snap_nod), rb + 4u * (1 + (uint32_t)ki) + 2u,
+            (uint16_t)cur_get<D>(x, ln, ki));
     pend = ((pw >> sh) & 0xffu) - 1;
   }
   PW(pi) = (pw & ~(0xffu << sh)) | (pend << sh);
@@ -448,10 +453,14 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       done = true;
     }
   }
-  XW(lay.x_pick + x.lane) = pick;
   // Queue.Pop (sim.go:85), counted at the sender: at most one per tick, so 16 bits each
   ln.pops += (pick & kPickValid) ? ((pick & kMarkerBit) ? 0x10000u : 1u) : 0u;
-  wave_sync();
+  // the unrolled receive phase reads pick words from the senders' lanes (ds_bpermute); the
+  // runtime-loop one, under divergent control flow, from the shared region
+  if constexpr (!(unrolled(D) && CLSNAP_B_PRED)) {
+    XW(lay.x_pick + x.lane) = pick;
+    wave_sync();
+  }
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
   if constexpr (unrolled(D) && CLSNAP_B_PRED) {
@@ -460,7 +469,9 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       if (ki >= lay.id) break;  // uniform: the layout holds id in-links per lane
       const uint32_t w = it[ki];
       const uint32_t src = w & 0xffu;
-      const uint32_t pk = XW(lay.x_pick + x.seg_base + src);
+      // the sender's pick word, read from its lane (ds_bpermute: no LDS store, no wave sync,
+      // and no LDS alias that would pin the read behind the marker path's stores)
+      const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x.seg_base + src) << 2), (int)pick);
       const bool m = act && ki < x.indeg && (pk & kPickValid) && ((pk >> 16) & 0x7fu) == ((w >> 8) & 0xffu);
       const bool mk = m && (pk & kMarkerBit);
       const bool tok = m && !mk;
@@ -512,12 +523,13 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       for (int32_t j = 0; j < D; ++j) {
         if (j >= x.outdeg) continue;
         push<D, STAGED>(x, ln, j, kMarkerBit | sid, k0 + j);
-        // the reference scans this sender's links after the push when the trigger came
-        // from a lower rank: a link that was empty at tick start gets peeked once more
-        if ((int32_t)src < x.v && ((empty_scanned >> j) & 1u)) {
-          ln.peek++;
-          empty_scanned &= ~(1u << j);
-        }
+      }
+      // the reference scans this sender's links after the pushes when the trigger came from
+      // a lower rank: every link that was empty at tick start gets peeked once more (once
+      // per tick: the first such trigger clears the mask)
+      if ((int32_t)src < x.v && empty_scanned) {
+        ln.peek += (uint32_t)__builtin_popcount(empty_scanned);
+        empty_scanned = 0;
       }
     }
     ln.draw += act ? (int32_t)total : 0;
@@ -676,9 +688,8 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   }
   const Ctx x{p, lay, X + lay.col + lane, X, sched, lrow, lane, seg * N, v, seg, ii, st,
               indeg, outdeg, valid ? (int32_t)nb[2] : 0,
-              4u * st * (uint32_t)N * (uint32_t)lay.rw,
-              (int32_t)(p.draws < 0x7fffffffLL ? p.draws : 0x7fffffffLL),
-              4ull * st * (uint64_t)N * (uint64_t)lay.rw < (1ull << 24)};
+              (4u * st * (uint32_t)N * (uint32_t)lay.rw) >> 8,
+              (int32_t)(p.draws < 0x7fffffffLL ? p.draws : 0x7fffffffLL)};
   InLinks<D> it;
   if constexpr (unrolled(D)) {
 #pragma unroll
