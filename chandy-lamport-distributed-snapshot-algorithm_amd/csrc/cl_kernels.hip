@@ -246,15 +246,19 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // are staged in LDS.  A compile-time choice: with an HBM delay load anywhere on the path
 // the compiler waits with s_waitcnt vmcnt(0) at the join, and on gfx950 vmcnt also counts
 // the wave's outstanding global STORES (snapshot outputs) -- a full store drain per push.
-template <int D, bool STAGED>
-__device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int32_t k) {
+// `pre`: the delay already read by the caller (PRE; a broadcast reads its delays together,
+// one LDS wait instead of one per push).
+template <int D, bool STAGED, bool PRE = false>
+__device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_t payload, int32_t k,
+                                     uint32_t pre = 0) {
   const Layout& lay = x.lay;
   if (k >= x.draws) { ln.flag = ST_DELAY_EXHAUSTED; return; }
   const uint32_t chw = hw_get<D>(x, ln, ko);
   const uint32_t cnt = chw >> 8;
   if (cnt >= (uint32_t)kMaxQueued) { ln.flag = ST_FIFO_OVERFLOW; return; }
   uint32_t delay;
-  if constexpr (STAGED) delay = x.lrow[k];
+  if constexpr (PRE) delay = pre;
+  else if constexpr (STAGED) delay = x.lrow[k];
   else delay = x.sched[(size_t)x.inst * x.p.sched_row + k];
   const uint32_t e = payload | ((uint32_t)(ln.time + 1 + (int32_t)delay) << 16);
   const uint32_t cap = 1u << lay.cap_log2;
@@ -519,10 +523,25 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       const uint32_t sid = tv >> 8;
       // exclusive prefix of the triggering sender within the instance
       const int32_t k0 = ln.draw + (int32_t)(XW(lay.x_off + x.seg_base + src) - (uint32_t)x.outdeg - base);
+      if constexpr (STAGED) {
+        // the broadcast's delays, read together (k0 + j may pass the schedule's end only in
+        // an instance that push() then freezes; the staged rows stay inside the wave's LDS)
+        uint32_t dl[D];
 #pragma unroll
-      for (int32_t j = 0; j < D; ++j) {
-        if (j >= x.outdeg) continue;
-        push<D, STAGED>(x, ln, j, kMarkerBit | sid, k0 + j);
+        for (int32_t j = 0; j < D; ++j) dl[j] = x.lrow[k0 + j];
+#pragma unroll
+        for (int32_t j = 0; j < D; ++j) asm volatile("" : "+v"(dl[j]));
+#pragma unroll
+        for (int32_t j = 0; j < D; ++j) {
+          if (j >= x.outdeg) continue;
+          push<D, STAGED, true>(x, ln, j, kMarkerBit | sid, k0 + j, dl[j]);
+        }
+      } else {
+#pragma unroll
+        for (int32_t j = 0; j < D; ++j) {
+          if (j >= x.outdeg) continue;
+          push<D, STAGED>(x, ln, j, kMarkerBit | sid, k0 + j);
+        }
       }
       // the reference scans this sender's links after the pushes when the trigger came from
       // a lower rank: every link that was empty at tick start gets peeked once more (once
