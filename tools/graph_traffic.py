@@ -15,7 +15,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RUN_KERNELS = {"k_reset", "k_hostops", "k_tally", "k_pick", "k_marker", "k_scan", "k_push",
+RUN_KERNELS = {"k_reset", "k_sn_reset", "k_hostops", "k_tally", "k_pick", "k_marker", "k_scan", "k_push",
                "k_drain_begin", "k_drain_ctl", "k_drain_end"}
 
 
