@@ -430,12 +430,17 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
         p.mlist[bk * kGThreads + atomicAdd(&s_m, 1)] = MDel{s, v, k, sid};
       } else {
         atomicAdd(&p.tokens[v], (int32_t)pay);  // HandleToken node.go:175
-        const uint32_t tc = p.tokcnt[k];
         if (p.hist) {
+          const uint32_t tc = p.tokcnt[k];
           if (tc < (uint32_t)p.hist) p.histv[(size_t)k * p.hist + tc] = pay;
           else set_status(p.sc, kGStatusHistOverflow);
+          p.tokcnt[k] = tc + 1;
+        } else {
+          // (one pop per sender and tick: k has no other writer; a non-returning add ends
+          // the lane's chain at the route load instead of waiting for a cursor read:
+          // C4 8.61-8.65 -> 8.61-8.62 ms, C5 4,352-4,367 -> 4,335-4,344 ms, gpurun_out/r04e)
+          atomicAdd(&p.tokcnt[k], 1u);
         }
-        p.tokcnt[k] = tc + 1;
       }
       break;
     }
