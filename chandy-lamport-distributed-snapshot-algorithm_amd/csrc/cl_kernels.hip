@@ -160,6 +160,14 @@ struct Lane {
 constexpr bool unrolled(int D) { return D <= CLSNAP_UNROLL_MAX; }
 template <int D>
 using InLinks = uint32_t[unrolled(D) ? D : 1];
+// The unrolled kernels hold each in-link as its match key: sender lane (bits 7..0) and the
+// pick word's valid bit and out-link index at the sender (the bits of kKeyMask).  kNoKey
+// (out-link 127 without the valid bit) matches no pick word.
+constexpr uint32_t kKeyMask = 0x407f0000u;
+constexpr uint32_t kNoKey = 0x007f0000u;
+__device__ __forceinline__ uint32_t in_key(uint32_t w) {
+  return (w & 0xffu) | ((w & 0x7f00u) << 8) | 0x40000000u;
+}
 // In-link recording cursors (delivered-token counts) of the unrolled kernels live in two
 // packed registers instead of the link words' hi16 halves (A/B knob): phase B's per-in-link
 // LDS read + write becomes one add.  The LDS halves are refreshed only for the state image.
@@ -476,9 +484,12 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       // the sender's pick word, read from its lane (ds_bpermute: no LDS store, no wave sync,
       // and no LDS alias that would pin the read behind the marker path's stores)
       const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x.seg_base + src) << 2), (int)pick);
-      const bool m = act && ki < x.indeg && (pk & kPickValid) && ((pk >> 16) & 0x7fu) == ((w >> 8) & 0xffu);
-      const bool mk = m && (pk & kMarkerBit);
-      const bool tok = m && !mk;
+      // one masked compare against the in-link's key (in_key): a valid pick on the out-link
+      // that feeds this in-link.  Lanes of inactive instances picked nothing (pick = 0), and
+      // in-links past the node's in-degree hold kNoKey, so neither needs its own test.
+      const bool m = ((pk ^ w) & kKeyMask) == 0u;
+      const bool mk = m && (int32_t)pk < 0;
+      const bool tok = m && (int32_t)pk >= 0;
       const uint32_t pay = pk & 0xffffu;
       if constexpr (TRACE)  // ReceivedMsgRecord (sim.go:86), the receiver's tokens before handling
         if (m) temit<TRACE>(x, mk ? TK_RECV_MARKER : TK_RECV_TOKEN, src, ln.time, src << 8, (int32_t)pay, ln.tokens);
@@ -712,7 +723,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   InLinks<D> it;
   if constexpr (unrolled(D)) {
 #pragma unroll
-    for (int32_t k = 0; k < D; ++k) it[k] = k < indeg ? nb[3 + k] : 0u;
+    for (int32_t k = 0; k < D; ++k) it[k] = k < indeg ? in_key(nb[3 + k]) : kNoKey;
   } else {
     it[0] = 0;
   }
