@@ -125,7 +125,6 @@ struct Lane {
   uint32_t started;
   int32_t time, draw, status;
   uint32_t peek, push;
-  uint32_t pops;  // packets this node delivered as a sender: tokens (lo16) | markers (hi16); <= 1 per tick
   uint32_t hw[2];   // (head words in registers, unrolled D <= 4) out-link k's head word: u16 k & 1 of word k >> 1
   uint32_t cur[2];  // (cursors in registers, unrolled D <= 4) in-link k's recording cursor: u16 k & 1 of word k >> 1
   bool alive;    // instance still running (uniform within the segment)
@@ -465,8 +464,6 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       done = true;
     }
   }
-  // Queue.Pop (sim.go:85), counted at the sender: at most one per tick, so 16 bits each
-  ln.pops += (pick & kPickValid) ? ((pick & kMarkerBit) ? 0x10000u : 1u) : 0u;
   // the unrolled receive phase reads pick words from the senders' lanes (ds_bpermute); the
   // runtime-loop one, under divergent control flow, from the shared region
   if constexpr (!(unrolled(D) && CLSNAP_B_PRED)) {
@@ -746,7 +743,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
     ln.tokens = valid ? (int32_t)topo[(size_t)N * p.topo_w + v] : 0;
     ln.started = 0;
     ln.time = ln.draw = ln.status = 0;
-    ln.peek = ln.pops = ln.push = 0;
+    ln.peek = ln.push = 0;
   } else {
     const uint32_t* S = p.state + ii;
     const uint32_t b = (uint32_t)v * (lay.priv + G_NUM);
@@ -758,7 +755,6 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
     ln.draw = valid ? (int32_t)R[G_DRAW * st] : 0;
     ln.status = valid ? (int32_t)R[G_STATUS * st] : 0;
     ln.peek = valid ? R[G_PEEK * st] : 0;
-    ln.pops = valid ? (R[G_POP_TOK * st] | (R[G_POP_MK * st] << 16)) : 0;
     ln.push = valid ? R[G_PUSH * st] : 0;
     wave_sync();
     if (valid && v == 0) {
@@ -827,21 +823,29 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
       // TICK: op.a ticks.  DRAIN: tick until every started snapshot completed (at most
       // op.a ticks, else HANG), then op.b more (test_common.go:123-137).  Per instance.
       const bool drain = op.kind == OP_DRAIN;
-      // (rem: ticks left to run after the wait; every waiting lane runs one tick per
-      // iteration, so the iteration count is its waiting ticks)
-      int32_t rem = drain ? op.b : op.a;
-      bool waiting = drain;
+      // A lane ticks while iter < until: op.a ticks, or (DRAIN) kNoUntil while it waits, and
+      // op.b more from the iteration whose check finds its snapshots complete.  Every waiting
+      // lane runs one tick per iteration, so the iteration count is its waiting ticks.  The
+      // wait check runs only while some lane of the wave waits (uniform), so the tick loop's
+      // control is one compare per iteration otherwise.
+      constexpr int32_t kNoUntil = 0x7fffffff;
+      int32_t until = drain ? kNoUntil : op.a;
+      bool anyw = drain;
       for (int32_t iter = 0;; ++iter) {
-        if (waiting && (!ln.alive || (int32_t)XW(lay.x_ndone + seg) >= n_started)) waiting = false;
-        if (waiting && iter >= op.a) {
-          ln.status = ST_HANG;
-          ln.alive = false;
-          waiting = false;
+        if (anyw) {
+          const bool w = until == kNoUntil;
+          if (w && (!ln.alive || (int32_t)XW(lay.x_ndone + seg) >= n_started)) {
+            until = iter + op.b;
+          } else if (w && iter >= op.a) {
+            ln.status = ST_HANG;
+            ln.alive = false;
+            until = iter;
+          }
+          anyw = __ballot(until == kNoUntil) != 0;
         }
-        const bool act = ln.alive && (waiting || rem > 0);
+        const bool act = ln.alive && iter < until;
         if (!__ballot(act)) break;
         tick<D, STAGED, TRACE>(x, ln, it, act);
-        if (act && !waiting) rem--;
       }
 #if CLSNAP_PROF
       PROF_ADD(ln, 4, ot0);
@@ -879,11 +883,28 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
       }
     }
   }
+  // Queue.Pop counts (sim.go:85), derived instead of counted per tick: every pop delivers to
+  // one receiver of the same instance in the same tick, so the instance's token pops are its
+  // in-links' recording cursors (one per delivered token packet) and its marker pops are, per
+  // started snapshot, indeg - pending (a creation's marker plus the later ones; an initiator
+  // starts at indeg pending).
+  uint32_t ptok = 0, pmk = 0;
+  if constexpr (unrolled(D)) {
+#pragma unroll
+    for (int32_t k = 0; k < D; ++k)
+      if (k < indeg) ptok += cur_get<D>(x, ln, k);
+  } else {
+    for (int32_t k = 0; k < indeg; ++k) ptok += CUR(k);
+  }
+  for (uint32_t m = ln.started; m; m &= m - 1u) {
+    const uint32_t sid = (uint32_t)__builtin_ctz(m);
+    pmk += (uint32_t)indeg - ((PW(lay.w_pend + (sid >> 2)) >> ((sid & 3u) * 8u)) & 0xffu);
+  }
   if (valid) {
     lds_u32* acc = &XW(lay.x_acc + 5 * seg);
     lds_add(acc + 0, ln.peek);
-    lds_add(acc + 1, ln.pops & 0xffffu);
-    lds_add(acc + 2, ln.pops >> 16);
+    lds_add(acc + 1, ptok);
+    lds_add(acc + 2, pmk);
     lds_add(acc + 3, ln.push);
     lds_add(acc + 4, (uint32_t)inflight);
   }
@@ -926,8 +947,8 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
   R[G_DRAW * st] = (uint32_t)ln.draw;
   R[G_STATUS * st] = (uint32_t)ln.status;
   R[G_PEEK * st] = ln.peek;
-  R[G_POP_TOK * st] = ln.pops & 0xffffu;
-  R[G_POP_MK * st] = ln.pops >> 16;
+  R[G_POP_TOK * st] = ptok;  // (informational: a continuation derives them again)
+  R[G_POP_MK * st] = pmk;
   R[G_PUSH * st] = ln.push;
   if (v == 0) {
     uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;

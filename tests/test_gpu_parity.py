@@ -288,6 +288,32 @@ def test_rerun_equals_flush_and_oracle(cfg):
                          status=status, times=times)
 
 
+def test_wait_snapshot_after_back_to_back_split_reruns():
+    """back-to-back split reruns leave the spill-capable half running on the
+    second stream, whose prologue resets completion ticks.  A collector's cl_wait_snapshot
+    (and cl_poll_snapshot) must join that stream before reading them: the wait returns at
+    once (CL_E_NOT_COMPLETE because some instances stopped FATAL, with every completed
+    instance counted) instead of waiting out its timeout on ticks of instances still
+    being replayed."""
+    import ctypes
+    import time
+    top, events, n = "8nodes.top", "8nodes-concurrent-snapshots.events", 8192
+    sim = engine_run(top, events, n, fifo_lds_slots=2)
+    spilled, split = sim.replay_split()
+    assert spilled > 0 and split > 0 and (sim.status() != cl.INST_OK).any()
+    want = [sim.poll_snapshot(sid) for sid in range(sim.num_snapshots)]
+    for sid in range(sim.num_snapshots):
+        sim.rerun()
+        sim.rerun()   # back to back: no join of the second stream in between
+        v = ctypes.c_int64(-1)
+        t0 = time.perf_counter()
+        rc = sim._L.cl_wait_snapshot(sim._h, sid, 0, n, 20_000, ctypes.byref(v))
+        waited = time.perf_counter() - t0
+        assert rc == -9 and v.value == want[sid] and waited < 10.0, (sid, rc, v.value, want[sid], waited)
+        sim.rerun()
+        assert sim.poll_snapshot(sid) == want[sid]
+
+
 def test_replay_plan_spill_free_and_split():
     """The first full run of a program is the probe: per-instance spill flags and final
     ticks.  A program that never spills replays wholly on the spill-free kernel; one in which
