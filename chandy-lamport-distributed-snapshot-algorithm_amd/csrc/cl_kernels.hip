@@ -288,6 +288,46 @@ __device__ __forceinline__ void push(const Ctx& x, Lane& ln, int32_t ko, uint32_
   ln.push++;
 }
 
+// push() as straight-line code: the FIFO entry is written to its ring slot, or -- when the
+// push does not land in the LDS ring (link past the out-degree, delay stream exhausted, ring
+// full) -- to this lane's pick word in the shared region, which is dead after phase B (phase
+// A writes it before any read).  SPILLOK: a full LDS ring spills to the HBM ring under a
+// (rare) branch, as push().  The failure flags follow push(): delay exhaustion first, then
+// overflow; a later link of the same broadcast still pushes.
+template <int D, bool SPILLOK>
+__device__ __forceinline__ void push_pred(const Ctx& x, Lane& ln, int32_t ko, bool on, uint32_t payload, int32_t k,
+                                          uint32_t delay) {
+  const Layout& lay = x.lay;
+  const uint32_t cap = 1u << lay.cap_log2;
+  const uint32_t chw = hw_get<D>(x, ln, ko);
+  const uint32_t cnt = chw >> 8;
+  const bool dly_ok = k < x.draws;
+  const bool live = on && dly_ok;
+  bool ok = live && cnt < cap;
+  const uint32_t e = payload | ((uint32_t)(ln.time + 1 + (int32_t)delay) << 16);
+  const uint32_t slot = lay.w_fifo + ((uint32_t)ko << lay.cap_log2) + ((chw + cnt) & (cap - 1));
+  *(ok ? &PW(slot) : &XW(lay.x_pick + x.lane)) = e;
+  if constexpr (SPILLOK) {
+    if (__builtin_expect(live && cnt >= cap, 0)) {  // LDS ring full: the HBM spill ring
+      if (lay.ocap_log2 >= 0 && cnt < (uint32_t)kMaxQueued && cnt - cap < (1u << lay.ocap_log2)) {
+        const uint32_t c = (uint32_t)(x.out_off + ko);
+        const uint32_t om = (1u << lay.ocap_log2) - 1;
+        uint32_t* hp = &x.p.ovh[c * x.stride + x.inst];
+        uint32_t h = 0;
+        if (cnt == cap) *hp = 0u;
+        else h = *hp;
+        x.p.ovf[((c << lay.ocap_log2) + ((h + cnt - cap) & om)) * x.stride + x.inst] = e;
+        if (x.p.spill_flag) x.p.spill_flag[x.inst] = 1;
+        ok = true;
+      }
+    }
+  }
+  if constexpr (hw_reg(D)) ln.hw[ko >> 1] += ok ? kCountOne << ((ko & 1) * 16) : 0u;
+  else hw_set<D>(x, ln, ko, ok ? chw + kCountOne : chw);
+  ln.push += ok ? 1u : 0u;
+  ln.flag = (on && !ok) ? (dly_ok ? (int32_t)ST_FIFO_OVERFLOW : (int32_t)ST_DELAY_EXHAUSTED) : ln.flag;
+}
+
 // CreateLocalSnapshot (node.go:58-84): record tokens and open every in-channel except
 // the one the first marker arrived on (arrive = -1 at the initiator).  A channel's
 // recording is the cursor interval [begin, end) over the tokens delivered on it.
@@ -364,21 +404,19 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
                                               uint32_t src, int32_t sid, int32_t& ntrig) {
   const Layout& lay = x.lay;
   const uint32_t pi = lay.w_pend + (sid >> 2), sh = (sid & 3) * 8;
-  const uint32_t pw = PW(pi);
-  uint32_t pend;
-  if (!((ln.started >> sid) & 1u)) {  // first marker: record, then broadcast (phase D)
+  const bool first = !((ln.started >> sid) & 1u);
+  if (first) {  // first marker: record, then broadcast (phase D)
     ln.started |= 1u << sid;
     create_local<D>(x, ln, it, sid, ki);
-    pend = (uint32_t)x.indeg - 1;
     if constexpr (TRACE)  // SendToNeighbors' SentMsgRecords (node.go:100)
       for (int32_t j = 0; j < x.outdeg; ++j)
         temit<TRACE>(x, TK_SENT_MARKER, (uint32_t)x.p.ch_dest[x.out_off + j], ln.time, (src << 8) | (1u + j), sid,
                      ln.tokens);
-    if (x.outdeg) {
-      XW(lay.x_tslot + x.seg_base + src) = (uint32_t)x.outdeg;
-      TRIG(ntrig) = (uint16_t)(src | ((uint32_t)sid << 8));
-      ntrig++;
-    }
+    // the broadcast's draw slot (0 for a node without out-links: the slot stays 0 and the
+    // trigger entry is not counted)
+    XW(lay.x_tslot + x.seg_base + src) = (uint32_t)x.outdeg;
+    TRIG(ntrig) = (uint16_t)(src | ((uint32_t)sid << 8));
+    ntrig += x.outdeg ? 1 : 0;
   } else {  // later marker: stop recording this channel
     // hi16 of the cursor word: the channel's end.  The record's offset is pinned in one
     // VGPR (empty asm) so the in-link's constant folds into the store's immediate offset
@@ -387,9 +425,12 @@ __device__ __forceinline__ void handle_marker(const Ctx& x, Lane& ln, const InLi
     asm volatile("" : "+v"(rb));
     st_snap(reinterpret_cast<uint16_t*>(x.p.snap_nod), rb + 4u * (1 + (uint32_t)ki) + 2u,
             (uint16_t)cur_get<D>(x, ln, ki));
-    pend = ((pw >> sh) & 0xffu) - 1;
   }
-  PW(pi) = (pw & ~(0xffu << sh)) | (pend << sh);
+  // the pending count (u8 field sh of word pi) in one LDS atomic: a creation sets it to
+  // indeg - 1 (the field is 0 before), a later marker takes one (the field is >= 1: a marker
+  // is still expected), so neither carries into the neighbouring fields
+  const uint32_t old = lds_add(&PW(pi), first ? (uint32_t)(x.indeg - 1) << sh : 0u - (1u << sh));
+  const uint32_t pend = first ? (uint32_t)(x.indeg - 1) : ((old >> sh) & 0xffu) - 1;
   if (pend == 0) {
     node_complete(x, ln, sid);
     temit<TRACE>(x, TK_END, 0u, ln.time, (src << 8) | 255u, sid, ln.tokens);  // sim.go:127
@@ -411,7 +452,7 @@ __device__ __forceinline__ void refill(const Ctx& x, int32_t ko, uint32_t slot) 
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
 // Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
 // it[] holds this node's in-link words.
-template <int D, bool STAGED, bool TRACE>
+template <int D, bool STAGED, bool TRACE, bool NOSPILL = false>
 __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
@@ -473,14 +514,21 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
   if constexpr (unrolled(D) && CLSNAP_B_PRED) {
+    // the senders' pick words, read from their lanes (ds_bpermute: no LDS store, no wave
+    // sync, no LDS alias that would pin the reads behind the marker path's stores), all
+    // issued before the first is used: one LDS round trip per tick, not one per in-link
+    uint32_t pks[D];
+#pragma unroll
+    for (int32_t ki = 0; ki < D; ++ki) {
+      if (ki >= lay.id) break;
+      pks[ki] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x.seg_base + (it[ki] & 0xffu)) << 2), (int)pick);
+    }
 #pragma unroll
     for (int32_t ki = 0; ki < D; ++ki) {
       if (ki >= lay.id) break;  // uniform: the layout holds id in-links per lane
       const uint32_t w = it[ki];
       const uint32_t src = w & 0xffu;
-      // the sender's pick word, read from its lane (ds_bpermute: no LDS store, no wave sync,
-      // and no LDS alias that would pin the read behind the marker path's stores)
-      const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x.seg_base + src) << 2), (int)pick);
+      const uint32_t pk = pks[ki];
       // one masked compare against the in-link's key (in_key): a valid pick on the out-link
       // that feeds this in-link.  Lanes of inactive instances picked nothing (pick = 0), and
       // in-links past the node's in-degree hold kNoKey, so neither needs its own test.
@@ -540,10 +588,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
 #pragma unroll
         for (int32_t j = 0; j < D; ++j) asm volatile("" : "+v"(dl[j]));
 #pragma unroll
-        for (int32_t j = 0; j < D; ++j) {
-          if (j >= x.outdeg) continue;
-          push<D, STAGED, true>(x, ln, j, kMarkerBit | sid, k0 + j, dl[j]);
-        }
+        for (int32_t j = 0; j < D; ++j) push_pred<D, !NOSPILL>(x, ln, j, j < x.outdeg, kMarkerBit | sid, k0 + j, dl[j]);
       } else {
 #pragma unroll
         for (int32_t j = 0; j < D; ++j) {
@@ -845,7 +890,7 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
         }
         const bool act = ln.alive && iter < until;
         if (!__ballot(act)) break;
-        tick<D, STAGED, TRACE>(x, ln, it, act);
+        tick<D, STAGED, TRACE, (CAP > 0 && !SPILL)>(x, ln, it, act);
       }
 #if CLSNAP_PROF
       PROF_ADD(ln, 4, ot0);

@@ -4,8 +4,9 @@
 #               8-GPU node (2^17 instances), c2, c4 and c5 (with their cpu baselines), and a
 #               2-rank gloo rehearsal of the multi-GPU path on one card
 #   PART=prof   exec-kernel PMC + kernel stats (c3, c3 at 2^17, c2: tools/make_profiles.py
-#               turns gpurun_out/pmc_* into profiles/); graph kernel stats (c4, c5) and graph
-#               HBM traffic (c4, c5 with the drain), summarised on the box
+#               turns gpurun_out/pmc_* into profiles/); graph kernel stats (c4, c5) and C4's
+#               HBM traffic, summarised on the box
+#   PART=c5traffic  C5's HBM traffic with the drain (two ~9-minute counter passes)
 # usage: TAG=r03f PART=bench bash tools/gpu_final.sh
 set -e
 R=$GRAFT_REPO_ROOT
@@ -35,10 +36,5 @@ else
   # only the traffic summaries come back, under $O/profiles)
   PMCG_ROOT=/tmp CFG=c4 bash tools/gpu_pmc_graph.sh
   PMCG_DIR=/tmp/pmcg_c4 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c4 1048576 80 > $O/traffic_c4.log
-  # C5's passes write nothing for minutes: a heartbeat file keeps the run visibly alive
-  ( while true; do date >> $O/heartbeat.log; sleep 30; done ) &
-  HB=$!
-  PASS_S=540 PMCG_ROOT=/tmp CFG=c5 bash tools/gpu_pmc_graph.sh || { kill $HB; exit 1; }
-  kill $HB
-  PMCG_DIR=/tmp/pmcg_c5 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c5 100000 4100 drain > $O/traffic_c5.log
+  # (C5's traffic passes run ~20 min: PART=c5traffic, a call of their own)
 fi
