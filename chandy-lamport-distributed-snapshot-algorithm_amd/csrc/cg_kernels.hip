@@ -53,15 +53,57 @@ __device__ inline void wave_count(unsigned long long* dst, unsigned long long x)
   if (lane_id() == 0 && x) atomicAdd(dst, x);
 }
 
+// Inclusive prefix sum of a 32-bit value over the wave (every lane active): DPP row shifts
+// and row broadcasts, no LDS permutes (a 64-bit __shfl tree costs two per step).
+__device__ inline uint32_t wave_incl_scan32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+__device__ inline uint32_t wave_total32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(v), 63);
+}
+
+// block_exclusive_scan2 for values whose block totals fit 32 bits (one tick's triggers and
+// sends): DPP wave scans.  sh: [2 * 16].
+__device__ inline void block_exclusive_scan2_32(uint32_t& a, uint32_t& b, uint32_t& tot_a, uint32_t& tot_b,
+                                                uint32_t* sh) {
+  const int lane = (int)lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t ia = wave_incl_scan32(a), ib = wave_incl_scan32(b);
+  if (lane == 63) {
+    sh[2 * w] = ia;
+    sh[2 * w + 1] = ib;
+  }
+  __syncthreads();
+  uint32_t pa = 0, pb = 0;
+  tot_a = tot_b = 0;
+  for (int k = 0; k < nw; ++k) {
+    if (k < w) {
+      pa += sh[2 * k];
+      pb += sh[2 * k + 1];
+    }
+    tot_a += sh[2 * k];
+    tot_b += sh[2 * k + 1];
+  }
+  __syncthreads();
+  a = pa + ia - a;
+  b = pb + ib - b;
+}
+
 // Block-reduce NV per-thread counts and add them to this block's counter shard.  Every
-// thread of the block must call it (it has a barrier).
+// thread of the block must call it (it has a barrier).  A thread's counts are small (one
+// tick's peeks, pops, pushes of one node), so the wave sums are 32-bit DPP reductions.
 template <int NV>
 __device__ inline void block_count(const GParams& p, const int (&idx)[NV], unsigned long long (&x)[NV]) {
   __shared__ unsigned long long sh[NV][kGThreads / 64];
   const int w = threadIdx.x >> 6;
   for (int i = 0; i < NV; ++i) {
-    x[i] = wave_sum(x[i]);
-    if (lane_id() == 0) sh[i][w] = x[i];
+    const uint32_t t = wave_total32((uint32_t)x[i]);
+    if (lane_id() == 0) sh[i][w] = t;
   }
   __syncthreads();
   if (threadIdx.x < NV) {
@@ -176,35 +218,17 @@ __device__ inline void complete_nodes(const GParams& p, bool done, int32_t sid, 
 // ---------------------------------------------------------------------------
 // block exclusive scan of (a, b) pairs over blockDim.x threads (multiple of 64)
 // ---------------------------------------------------------------------------
+__device__ inline void block_exclusive_scan2_32(uint32_t& a, uint32_t& b, uint32_t& tot_a, uint32_t& tot_b,
+                                                uint32_t* sh);
+// (every caller's block totals fit 32 bits: one tick's triggers, sends, in-degree sums)
 __device__ inline void block_exclusive_scan2(long long& a, long long& b, long long& tot_a, long long& tot_b,
                                              long long* sh /* [2 * 16] */) {
-  const int lane = (int)lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  long long ia = a, ib = b;
-  for (int o = 1; o < 64; o <<= 1) {
-    const long long xa = __shfl_up(ia, o), xb = __shfl_up(ib, o);
-    if (lane >= o) {
-      ia += xa;
-      ib += xb;
-    }
-  }
-  if (lane == 63) {
-    sh[2 * w] = ia;
-    sh[2 * w + 1] = ib;
-  }
-  __syncthreads();
-  long long pa = 0, pb = 0;
-  tot_a = tot_b = 0;
-  for (int k = 0; k < nw; ++k) {
-    if (k < w) {
-      pa += sh[2 * k];
-      pb += sh[2 * k + 1];
-    }
-    tot_a += sh[2 * k];
-    tot_b += sh[2 * k + 1];
-  }
-  __syncthreads();
-  a = pa + ia - a;
-  b = pb + ib - b;
+  uint32_t a32 = (uint32_t)a, b32 = (uint32_t)b, ta, tb;
+  block_exclusive_scan2_32(a32, b32, ta, tb, reinterpret_cast<uint32_t*>(sh));
+  a = a32;
+  b = b32;
+  tot_a = ta;
+  tot_b = tb;
 }
 
 // Block tally of node rank v = blockIdx.x * kGThreads + threadIdx.x: `trig` draws
@@ -215,6 +239,28 @@ __device__ inline int32_t tally_send_bit(const GParams& p, int32_t b, int32_t st
   const int v = b * kGThreads + threadIdx.x;
   int32_t j;
   return v < p.n && traffic_send(p, step, v, p.out_off[v + 1] - p.out_off[v], p.tokens[v], &j) ? 1 : 0;
+}
+
+// The tally of a block without broadcast triggers (no marker delivered by its senders):
+// the send bits' exclusive prefix from ballots, one barrier.
+__device__ inline void tally_sends(const GParams& p, int32_t bk, int32_t sendbit) {
+  __shared__ int s_w[kGThreads / 64];
+  const int v = bk * kGThreads + threadIdx.x, w = threadIdx.x >> 6;
+  const unsigned long long m = __ballot(sendbit != 0);
+  const uint32_t lane = lane_id();
+  const int excl = __popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) s_w[w] = __popcll(m);
+  __syncthreads();
+  int pre = 0, tot = 0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+    pre += k < w ? s_w[k] : 0;
+    tot += s_w[k];
+  }
+  if (sendbit) p.lsend[v] = pre + excl;
+  if (threadIdx.x == 0) {
+    p.bsum[2 * bk] = 0;
+    p.bsum[2 * bk + 1] = tot;
+  }
 }
 
 __device__ inline void tally(const GParams& p, int32_t bk, int32_t trig, int32_t sendbit) {
@@ -485,7 +531,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   __shared__ int32_t s_ctsum[kGThreads];
   __shared__ long long s_sh[2 * (kGThreads / 64)];
   if (!REMOTE && nm == 0 && !p.part) {  // no markers delivered by this block's senders: the tally only
-    tally(p, bk, 0, sendbit);
+    tally_sends(p, bk, sendbit);
     return;
   }
   s_trig[threadIdx.x] = 0;
@@ -599,6 +645,11 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t 
   // the first chunk of block tallies is loaded while the status check is in flight (one
   // latency, not two: this single-workgroup kernel is pure latency, ~6 us per tick)
   long long pa[PER], pb[PER];
+  unsigned long long d0 = 0, dp = 0;  // (thread 0: the draw counter, loaded with the tallies)
+  if (threadIdx.x == 0 && !p.part) {
+    d0 = p.sc->draw;
+    dp = p.sc->draw_pend;
+  }
   {
     const int i0 = p.blk_lo + PER * threadIdx.x;
 #pragma unroll
@@ -612,7 +663,7 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t 
     if (targ < 0 && threadIdx.x == 0) drain_decide(p, n_before, max_drain, (-1 - targ) ^ 1);  // (stays frozen)
     return;
   }
-  __shared__ long long sh[32];
+  __shared__ uint32_t sh[32];
   long long carry_a = 0, carry_b = 0;
   for (int c0 = p.blk_lo; c0 < p.blk_hi; c0 += PER * blockDim.x) {
     const int i0 = c0 + PER * threadIdx.x;
@@ -624,10 +675,10 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t 
       a += va[q];
       b += vb[q];
     }
-    long long ta, tb;
-    block_exclusive_scan2(a, b, ta, tb, sh);
-    a += carry_a;
-    b += carry_b;
+    uint32_t a32 = (uint32_t)a, b32 = (uint32_t)b, ta, tb;  // (a tick's totals fit 32 bits)
+    block_exclusive_scan2_32(a32, b32, ta, tb, sh);
+    a = (long long)a32 + carry_a;
+    b = (long long)b32 + carry_b;
     for (int q = 0; q < PER; ++q) {
       if (i0 + q < p.blk_hi) {
         p.bsum[2 * (i0 + q)] = a;
@@ -643,8 +694,8 @@ __global__ void __launch_bounds__(1024) k_scan(GParams p, int32_t targ, int32_t 
     p.sc->tot_trig = (unsigned long long)carry_a;
     p.sc->tot_send = (unsigned long long)carry_b;
   } else if (threadIdx.x == 0) {
-    fold_draw(p.sc);
-    const unsigned long long d = p.sc->draw;
+    const unsigned long long d = d0 + dp;  // fold_draw with the prefetched words
+    if (dp) p.sc->draw_pend = 0;
     p.sc->base_trig = d;
     p.sc->base_send = d + (unsigned long long)carry_a;
     p.sc->draw = d + (unsigned long long)(carry_a + carry_b);
