@@ -68,6 +68,31 @@ __device__ inline uint32_t wave_total32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(v), 63);
 }
 
+// Exclusive block scan of N 32-bit values per thread (block totals fit 32 bits): one DPP
+// wave scan per value, one LDS exchange.  sh: [N * 16].
+template <int N>
+__device__ inline void block_exclusive_scan_n32(uint32_t (&v)[N], uint32_t (&tot)[N], uint32_t* sh) {
+  const int lane = (int)lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t inc[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    inc[i] = wave_incl_scan32(v[i]);
+    if (lane == 63) sh[N * w + i] = inc[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    uint32_t pre = 0, t = 0;
+    for (int k = 0; k < nw; ++k) {
+      pre += k < w ? sh[N * k + i] : 0u;
+      t += sh[N * k + i];
+    }
+    v[i] = pre + inc[i] - v[i];
+    tot[i] = t;
+  }
+  __syncthreads();
+}
+
 // block_exclusive_scan2 for values whose block totals fit 32 bits (one tick's triggers and
 // sends): DPP wave scans.  sh: [2 * 16].
 __device__ inline void block_exclusive_scan2_32(uint32_t& a, uint32_t& b, uint32_t& tot_a, uint32_t& tot_b,
@@ -520,24 +545,24 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   const bool pre = !REMOTE && p.n < kMarkerPrefetchBelow;
   MDel mpre{};
   if (pre) mpre = list[threadIdx.x];
-  if (block_frozen(p, targ)) return;
   __shared__ int s_nb, s_base;
   __shared__ int s_trig[kGThreads];
+  __shared__ int32_t s_ctsum[kGThreads];
+  // (cleared before the status check: its barrier orders them before any use)
+  s_trig[threadIdx.x] = 0;
+  s_ctsum[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_nb = 0;
+  if (block_frozen(p, targ)) return;
   // local snapshots created by this block's markers at nodes of in-degree <= kSmallIndeg,
   // expanded over their in-links by the whole block: (creation, in-link) pairs are
   // numbered by an exclusive prefix over the in-degrees
   __shared__ BigX s_cx[kGThreads];
   __shared__ int32_t s_cpre[kGThreads];
-  __shared__ int32_t s_ctsum[kGThreads];
-  __shared__ long long s_sh[2 * (kGThreads / 64)];
+  __shared__ uint32_t s_sh[4 * (kGThreads / 64)];
   if (!REMOTE && nm == 0 && !p.part) {  // no markers delivered by this block's senders: the tally only
     tally_sends(p, bk, sendbit);
     return;
   }
-  s_trig[threadIdx.x] = 0;
-  s_ctsum[threadIdx.x] = 0;
-  if (threadIdx.x == 0) s_nb = 0;
-  __syncthreads();
   unsigned long long c[2] = {0, 0};  // recorded, completed
   bool done = false;
   int32_t sid = 0, vdone = 0;
@@ -593,10 +618,22 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   complete_nodes(p, done, sid, vdone, t, c[1]);
   const int idx[2] = {GC_RECORDED, GC_COMPLETED};
   block_count<2>(p, idx, c);  // (has a barrier: s_trig and s_nb are final below)
-  // creations numbered in thread order (b), in-link pairs by the prefix of in-degrees (a)
+  // one block scan for both: creations numbered in thread order (b), in-link pairs by the
+  // prefix of in-degrees (a); and the tally (triggers c, traffic sends d)
   const bool cre = cslot >= 0;
-  long long a = cre ? (long long)(bx.hi - bx.lo) : 0, b = cre ? 1 : 0, tot, nc;
-  block_exclusive_scan2(a, b, tot, nc, s_sh);
+  const int32_t trig = s_trig[threadIdx.x];
+  uint32_t sv4[4] = {cre ? (uint32_t)(bx.hi - bx.lo) : 0u, cre ? 1u : 0u, (uint32_t)trig, (uint32_t)sendbit}, tv4[4];
+  block_exclusive_scan_n32<4>(sv4, tv4, s_sh);
+  const long long a = sv4[0], b = sv4[1], tot = tv4[0], nc = tv4[1];
+  if (!p.part) {  // (the partitioned mode tallies after the exchange, k_tally)
+    const int v = bk * kGThreads + threadIdx.x;
+    if (trig) p.ltrig[v] = (int32_t)sv4[2];
+    if (sendbit) p.lsend[v] = (int32_t)sv4[3];
+    if (threadIdx.x == 0) {
+      p.bsum[2 * bk] = tv4[2];
+      p.bsum[2 * bk + 1] = tv4[3];
+    }
+  }
   if (cre) {
     cslot = (int)b;
     s_cx[cslot] = bx;
@@ -618,8 +655,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
   __syncthreads();
   if (cslot >= 0) p.sn[(size_t)bx.sid * p.n + bx.v].stok = p.tokens[bx.v] - s_ctsum[cslot];
   if (threadIdx.x == 0 && s_nb) s_base = atomicAdd(&p.sc->big_n, s_nb);
-  if (!p.part) tally(p, bk, s_trig[threadIdx.x], sendbit);  // (has a barrier: s_base is final below)
-  else __syncthreads();
+  __syncthreads();
   if (bslot >= 0) p.big[s_base + bslot] = bx;
 }
 
@@ -917,6 +953,9 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
       if (jl == 0) q0 = p.hq[ob + tj];
     }
   }
+  // the high in-degree creations to expand at the end (k_marker's count, final before this
+  // launch): loaded with the rest, not one round trip after the pushes
+  const int nb = p.sc->big_n;
   long long ta0 = 0, tb0 = 0, ta1 = 0, tb1 = 0;  // (FUSED) this thread's two block tallies
   if constexpr (FUSED) {
     const int32_t i0 = 2 * (int32_t)threadIdx.x;
@@ -983,7 +1022,6 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
   // expansion of the local snapshots created at high in-degree nodes: the (creation,
   // in-link) pairs of each staged chunk are numbered by an LDS prefix over in-degrees and
   // dealt round-robin to every thread of the grid
-  const int nb = p.sc->big_n;
   constexpr int kChunk = 2 * kGThreads;  // descriptors staged in LDS at a time (16 KB)
   __shared__ BigX sx[kChunk];
   __shared__ int32_t spre[kChunk + 1];

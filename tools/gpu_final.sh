@@ -7,6 +7,7 @@
 #               turns gpurun_out/pmc_* into profiles/); graph kernel stats (c4, c5) and C4's
 #               HBM traffic, summarised on the box
 #   PART=c5traffic  C5's HBM traffic with the drain (two ~9-minute counter passes)
+#   PART=graph  the graph lines, kernel stats and C4 traffic only (after a graph-engine change)
 # usage: TAG=r03f PART=bench bash tools/gpu_final.sh
 set -e
 R=$GRAFT_REPO_ROOT
@@ -18,6 +19,14 @@ if [ "${PART:-bench}" = c5traffic ]; then
   PASS_S=540 PMCG_ROOT=/tmp CFG=c5 bash tools/gpu_pmc_graph.sh || { kill $HB; exit 1; }
   kill $HB
   PMCG_DIR=/tmp/pmcg_c5 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c5 100000 4100 drain > $O/traffic_c5.log
+elif [ "${PART:-bench}" = graph ]; then
+  # the graph configs again after a graph-engine change: bench lines, kernel stats, C4 traffic
+  timeout -k 10 300 python -u bench.py --config c4 --steps 10 --warmup 2 > $O/bench_c4.json 2> $O/bench_c4.err
+  timeout -k 10 300 python -u bench.py --config c5 --steps 1 --warmup 1 > $O/bench_c5.json 2> $O/bench_c5.err
+  CFG=c4 ARGS="--steps 3 --warmup 1" bash tools/gpu_prof_graph.sh
+  CFG=c5 ARGS="--steps 1 --warmup 1" bash tools/gpu_prof_graph.sh
+  PMCG_ROOT=/tmp CFG=c4 bash tools/gpu_pmc_graph.sh
+  PMCG_DIR=/tmp/pmcg_c4 OUT_DIR=$O/profiles python3 tools/graph_traffic.py c4 1048576 80 > $O/traffic_c4.log
 elif [ "${PART:-bench}" = bench ]; then
   timeout -k 10 300 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.err
   timeout -k 10 300 python -u bench.py --instances 131072 --no-cpu-baseline > $O/bench_c3_s17.json 2> $O/bench_c3_s17.err
