@@ -72,8 +72,8 @@ struct PDel {
 // Receiver-side channel state is one word per in-channel, tokcnt[k]: the tokens delivered on
 // it so far (the recording cursor).  A local snapshot created this tick learns whether its
 // in-channel k also delivered this tick, and what, from the SENDER's delivery word: sender
-// s = in_src[k] popped on out-link in_oj[k] this tick iff pick[s] == (t << 6) | in_oj[k],
-// with payload ppay[s] (each sender delivers at most once per tick, sim.go:90).
+// s = in_src[k] popped on out-link in_oj[k] this tick iff pp[s].x == (t << 6) | in_oj[k],
+// with payload pp[s].y (each sender delivers at most once per tick, sim.go:90).
 
 constexpr uint32_t kEmpty = 0xffffffffu;  // head receiveTime word of an empty channel
 
@@ -165,8 +165,10 @@ struct GParams {
   const uint8_t* in_oj;     // [e] out-link index at the sender of in-position k
   // node state
   int32_t* tokens;     // [n]
-  int32_t* pick;       // [n] (tick << 6) | out-index popped in that tick
-  uint32_t* ppay;      // [n] payload word of that pop (kGMarker | sid, or token count)
+  // [n] the sender's delivery word: x = (tick << 6) | out-index popped in that tick, y = the
+  // payload word of that pop (kGMarker | sid, or token count) -- one 8-byte entry, so a
+  // creation's expansion reads one line per in-link's sender, not two
+  int2* pp;
   int32_t* ltrig;      // [n] block-local exclusive prefix of triggered broadcasts (draws)
   int32_t* lsend;      // [n] block-local exclusive prefix of traffic sends
   long long* bsum;     // [2 * n_pblocks] block sums (trig, send) -> exclusive block offsets

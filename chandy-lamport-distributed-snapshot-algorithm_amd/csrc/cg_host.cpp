@@ -163,9 +163,10 @@ struct cl_graph {
   int64_t sched_len = 0;
   GBuf<int32_t> d_out_off, d_in_off, d_in_src, d_init_tok;
   GBuf<int2> d_route;
-  GBuf<int32_t> d_tokens, d_pick, d_ltrig, d_lsend, d_crn, d_mcnt;
+  GBuf<int32_t> d_tokens, d_ltrig, d_lsend, d_crn, d_mcnt;
+  GBuf<int2> d_pp;
   GBuf<MDel> d_mlist;
-  GBuf<uint32_t> d_tokcnt, d_ppay;
+  GBuf<uint32_t> d_tokcnt;
   GBuf<uint8_t> d_in_oj;
   GBuf<BigX> d_big;
   GBuf<unsigned long long> d_cpart;
@@ -209,11 +210,11 @@ struct cl_graph {
     (void)hipStreamSynchronize(stream);
     if (own_stream != stream) (void)hipStreamSynchronize(own_stream);
     GBuf<int32_t>* i32s[] = {&d_out_off, &d_in_off, &d_in_src, &d_init_tok, &d_tokens,
-                             &d_pick,    &d_ltrig,  &d_lsend,    &d_crn,    &d_mcnt,
+                             &d_ltrig,  &d_lsend,    &d_crn,    &d_mcnt,
                              &d_done,    &d_ctick};
     for (auto* b : i32s) b->release();
     d_cre.release(); d_bsum.release(); d_hq.release(); d_histv.release(); d_mlist.release(); d_route.release();
-    d_tokcnt.release(); d_ppay.release(); d_in_oj.release(); d_fifo.release(); d_sn.release(); d_rec.release(); d_sc.release(); d_ops.release();
+    d_tokcnt.release(); d_pp.release(); d_in_oj.release(); d_fifo.release(); d_sn.release(); d_rec.release(); d_sc.release(); d_ops.release();
     d_sched.release(); d_scratch.release(); d_big.release(); d_cpart.release();
     d_trace.release(); d_trace_cnt.release();
     d_outbox.release(); d_inbox.release(); d_out_n.release(); d_rmlist.release(); d_reports.release();
@@ -464,11 +465,11 @@ struct cl_graph {
     if ((uint64_t)s_cap * N >= (1ull << 40) || (uint64_t)s_cap * E >= (1ull << 40))
       return gerr(CL_E_LIMIT, "snapshot state too large");
     int rc;
-    if ((rc = d_tokens.ensure(N)) || (rc = d_pick.ensure(N)) || (rc = d_ltrig.ensure(N)) ||
+    if ((rc = d_tokens.ensure(N)) || (rc = d_pp.ensure(N)) || (rc = d_ltrig.ensure(N)) ||
         (rc = d_lsend.ensure(N)) || (rc = d_crn.ensure(N)) || (rc = d_mlist.ensure(NP * kGThreads)) ||
         (rc = d_mcnt.ensure(NP)) || (rc = d_big.ensure(N)) || (rc = d_cpart.ensure((size_t)kParts * kNumCnt)) ||
         (rc = d_cre.ensure(E)) || (rc = d_bsum.ensure(2 * NP)) || (rc = d_hq.ensure(E)) ||
-        (rc = d_tokcnt.ensure(E)) || (rc = d_ppay.ensure(N)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
+        (rc = d_tokcnt.ensure(E)) || (rc = d_histv.ensure(hist ? E * hist : 1)) ||
         (rc = d_fifo.ensure(E << cap_log2)) || (rc = d_sn.ensure(s_cap * N)) ||
         (rc = d_rec.ensure(s_cap * E)) ||
         (rc = d_done.ensure((size_t)s_cap * (1 + NP))) || (rc = d_ctick.ensure(s_cap)) || (rc = d_sc.ensure(1)) ||
@@ -521,7 +522,7 @@ struct cl_graph {
     p.in_off = d_in_off.p;
     p.in_src = d_in_src.p;
     p.tokens = d_tokens.p;
-    p.pick = d_pick.p;
+    p.pp = d_pp.p;
     p.ltrig = d_ltrig.p;
     p.lsend = d_lsend.p;
     p.bsum = d_bsum.p;
@@ -534,7 +535,6 @@ struct cl_graph {
     p.hq = d_hq.p;
     p.fifo = d_fifo.p;
     p.tokcnt = d_tokcnt.p;
-    p.ppay = d_ppay.p;
     p.in_oj = d_in_oj.p;
     p.histv = d_histv.p;
     p.sn = d_sn.p;
@@ -1273,7 +1273,7 @@ int cl_graph_device_bytes(cl_graph* g, int64_t* bytes) {
   if (!bytes) return gerr(CL_E_INVALID, "null output");
   size_t b = 0;
   b += g->d_out_off.bytes() + g->d_route.bytes() + g->d_in_off.bytes() +
-       g->d_in_src.bytes() + g->d_init_tok.bytes() + g->d_tokens.bytes() + g->d_pick.bytes() + g->d_tokcnt.bytes() + g->d_ppay.bytes() + g->d_in_oj.bytes() +
+       g->d_in_src.bytes() + g->d_init_tok.bytes() + g->d_tokens.bytes() + g->d_pp.bytes() + g->d_tokcnt.bytes() + g->d_in_oj.bytes() +
        g->d_ltrig.bytes() + g->d_lsend.bytes() + g->d_crn.bytes() + g->d_mlist.bytes() + g->d_mcnt.bytes() +
        g->d_big.bytes() + g->d_cpart.bytes() +
        g->d_cre.bytes() + g->d_bsum.bytes() + g->d_hq.bytes() +

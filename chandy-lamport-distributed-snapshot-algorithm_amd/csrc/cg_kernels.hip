@@ -314,8 +314,9 @@ __device__ inline int expand_range(const GParams& p, int32_t t, int32_t s0, int3
     bool closed = k == karr;  // the arriving channel does not record (node.go:66-69)
     const int32_t src = p.in_src[k];
     // (pick and payload loaded together: one dependent round trip after in_src, not two)
-    const int32_t pk = p.pick[src];
-    const uint32_t pay = p.ppay[src];
+    const int2 dw = p.pp[src];
+    const int32_t pk = dw.x;
+    const uint32_t pay = (uint32_t)dw.y;
     if (src > s0 && pk == ((t << 6) | (int32_t)p.in_oj[k])) {  // a later delivery this tick
       if (!(pay & kGMarker)) {
         b -= 1;  // delivered after the creating marker: recorded
@@ -396,7 +397,7 @@ __global__ void k_reset(GParams p, const int32_t* init_tok) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i < (size_t)p.n) {
     p.tokens[i] = init_tok[i];
-    p.pick[i] = -1;
+    p.pp[i].x = -1;
     p.crn[i] = 0;
   }
   if (i < (size_t)p.e) {
@@ -483,8 +484,7 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
       const uint32_t pay = (uint32_t)p.fifo[ring + head];
       const uint32_t nrt = cnt ? (uint32_t)(p.fifo[ring + ((head + 1) & capm)] >> 32) : kEmpty;
       p.hq[ch] = ((uint64_t)(((head + 1) & capm) | (cnt << 16)) << 32) | nrt;
-      p.pick[s] = (t << 6) | j;
-      p.ppay[s] = pay;
+      p.pp[s] = make_int2((t << 6) | j, (int)pay);
       const int32_t v = rte.x, k = rte.y;
       ++c[(pay & kGMarker) ? 2 : 1];
       if (v < p.part_lo || v >= p.part_hi) {  // partitioned: the receiver's device applies it
@@ -818,7 +818,7 @@ __device__ inline void push_node_reg(const GParams& p, const Bases& bs, int32_t 
       if (r == 0 && s0 < v) {
         // The reference delivers s0's marker before v's own turn in this tick, so v's
         // scan peeks the queues the broadcast makes non-empty (sim.go:82-84).
-        const int pk = p.pick[v];
+        const int pk = p.pp[v].x;
         const int pj = (pk >> 6) == t ? (pk & 63) : 64;
 #pragma unroll
         for (int j = 0; j < R; ++j)
@@ -864,7 +864,7 @@ __device__ inline void push_node_lanes(const GParams& p, const Bases& bs, int32_
     uint64_t cr[kRegCre];
 #pragma unroll
     for (int i = 0; i < kRegCre; ++i) cr[i] = i < ncre ? p.cre[lo + i] : ~0ull;
-    const int pk = p.pick[v];
+    const int pk = p.pp[v].x;
     auto cswap = [](uint64_t& a, uint64_t& b) {
       const uint64_t x = a < b ? a : b, y = a < b ? b : a;
       a = x;
@@ -906,7 +906,7 @@ __device__ inline void push_node_lanes(const GParams& p, const Bases& bs, int32_
       const uint32_t sid = (uint32_t)best;
       if (r == 0 && s0 < v) {
         // v's own scan peeks the queues s0's broadcast made non-empty (sim.go:82-84)
-        const int pk = p.pick[v];
+        const int pk = p.pp[v].x;
         const int pj = (pk >> 6) == t ? (pk & 63) : 64;
         if (j < pj && (uint32_t)q == kEmpty) ++c[1];
       }
@@ -1200,8 +1200,7 @@ __global__ void __launch_bounds__(kGThreads) k_sg_apply(GParams p, int32_t time,
 // staged for k_marker<true>).  Every channel carries at most one delivery per tick.
 __device__ inline void apply_delivery(const GParams& p, int32_t t, const PDel d) {
   // the remote sender's delivery word, on this device, for the expansions here
-  p.pick[d.s] = (t << 6) | (int32_t)p.in_oj[d.k];
-  p.ppay[d.s] = d.pay;
+  p.pp[d.s] = make_int2((t << 6) | (int32_t)p.in_oj[d.k], (int)d.pay);
   if (d.pay & kGMarker) {
     const int32_t sid = (int32_t)(d.pay & kGPayload);
     atomicMin(&p.sn[(size_t)sid * p.n + d.v].W, ((unsigned long long)t << 32) | (uint32_t)d.s);
