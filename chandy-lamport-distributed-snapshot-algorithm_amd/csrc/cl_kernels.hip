@@ -4,13 +4,15 @@
 // independent simulator instances.  Node-parallel layout: an instance of N nodes is a
 // segment of N consecutive lanes of a 64-lane wave (lane = node rank), 64/N instances
 // per wave, 4 independent waves per workgroup.  A node's mutable state lives in its
-// lane: tokens and the STARTED mask in VGPRs; its out-channel FIFOs (sender side), its
-// in-channel recording cursors (receiver side) and its per-snapshot pending counters in
-// the lane's private LDS column (word k at lds[k*64 + lane]: conflict-free for any
-// per-lane index).  Lanes exchange only three things per tick, through a small shared
-// LDS region: the packet each sender picked, the marker-broadcast draw counts, and their
-// exclusive prefix sums.  HBM carries the delay schedule (1 B per draw) and the snapshot
-// outputs.
+// lane: tokens and the STARTED mask in VGPRs (for degree bounds <= 4 also its out-links'
+// head words, in-links' recording cursors and in-link match keys); its out-channel FIFOs,
+// per-snapshot pending counters and trigger entries in the lane's private LDS column
+// (word k at lds[k*64 + lane]: conflict-free for any per-lane index).  Lanes exchange
+// three things per tick: the packet each sender picked (ds_bpermute reads of the sender's
+// lane; the runtime-loop kernels of large degree bounds through a shared LDS region), the
+// marker-broadcast draw counts and their exclusive prefix sums (shared LDS region, DPP
+// scan).  HBM carries the delay schedule (1 B per draw, staged in LDS per wave) and the
+// snapshot outputs.
 //
 // One tick (sim.go:71-95) in four wave-synchronous phases:
 //   A pick     every sender scans its out-links in dest order and pops the first due head
