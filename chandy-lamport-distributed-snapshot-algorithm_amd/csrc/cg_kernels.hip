@@ -95,6 +95,7 @@ __device__ inline void block_exclusive_scan_n32(uint32_t (&v)[N], uint32_t (&tot
 
 // block_exclusive_scan2 for values whose block totals fit 32 bits (one tick's triggers and
 // sends): DPP wave scans.  sh: [2 * 16].
+template <bool TRAIL = true>  // TRAIL: a barrier after the exchange (sh reused at once)
 __device__ inline void block_exclusive_scan2_32(uint32_t& a, uint32_t& b, uint32_t& tot_a, uint32_t& tot_b,
                                                 uint32_t* sh) {
   const int lane = (int)lane_id(), w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -114,7 +115,7 @@ __device__ inline void block_exclusive_scan2_32(uint32_t& a, uint32_t& b, uint32
     tot_a += sh[2 * k];
     tot_b += sh[2 * k + 1];
   }
-  __syncthreads();
+  if constexpr (TRAIL) __syncthreads();
   a = pa + ia - a;
   b = pb + ib - b;
 }
@@ -243,6 +244,7 @@ __device__ inline void complete_nodes(const GParams& p, bool done, int32_t sid, 
 // ---------------------------------------------------------------------------
 // block exclusive scan of (a, b) pairs over blockDim.x threads (multiple of 64)
 // ---------------------------------------------------------------------------
+template <bool TRAIL>
 __device__ inline void block_exclusive_scan2_32(uint32_t& a, uint32_t& b, uint32_t& tot_a, uint32_t& tot_b,
                                                 uint32_t* sh);
 // (every caller's block totals fit 32 bits: one tick's triggers, sends, in-degree sums)
@@ -453,16 +455,19 @@ __global__ void __launch_bounds__(kGThreads) k_pick(GParams p, int32_t targ) {
     const int32_t i = threadIdx.x + k * kGThreads;
     tmp[k] = i < nst ? p.hq[blo + i] : 0;
   }
-  if (block_frozen(p, targ)) return;
-  if (threadIdx.x == 0) s_m = 0;
-  {
+  // the status check shares the stage's barrier (block_frozen's rule: one value per block)
+  __shared__ int s_frozen;
+  if (threadIdx.x == 0) {
+    s_frozen = p.sc->status | (targ >= 0 ? p.sc->skip : p.sc->dskip[-1 - targ]);
+    s_m = 0;
+  }
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int32_t i = threadIdx.x + k * kGThreads;
-      if (i < nst) s_hq[i] = tmp[k];
-    }
+  for (int k = 0; k < kPer; ++k) {
+    const int32_t i = threadIdx.x + k * kGThreads;
+    if (i < nst) s_hq[i] = tmp[k];
   }
   __syncthreads();
+  if (s_frozen) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     p.sc->time = t;  // time++ (sim.go:72)
     p.sc->big_n = 0;
@@ -957,6 +962,8 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
   // launch): loaded with the rest, not one round trip after the pushes
   const int nb = p.sc->big_n;
   long long ta0 = 0, tb0 = 0, ta1 = 0, tb1 = 0;  // (FUSED) this thread's two block tallies
+  // (FUSED) the draw counter, folded by this tick's k_pick, written by no block of this kernel
+  const unsigned long long d0 = FUSED ? p.sc->draw : 0ull;
   if constexpr (FUSED) {
     const int32_t i0 = 2 * (int32_t)threadIdx.x;
     if (i0 < p.n_pblocks) {
@@ -975,12 +982,14 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
   }
   Bases bs{0ull, 0ull, p.bsum};
   __shared__ long long s_pre[FUSED ? 2 * kFuseBlocks : 2];
-  __shared__ unsigned long long s_base[2];
   if constexpr (FUSED) {
-    __shared__ long long s_sh[2 * (kGThreads / 64)];
+    __shared__ uint32_t s_sh[2 * (kGThreads / 64)];
     const int32_t i0 = 2 * (int32_t)threadIdx.x;
-    long long a = ta0 + ta1, b = tb0 + tb1, tot_a, tot_b;
-    block_exclusive_scan2(a, b, tot_a, tot_b, s_sh);
+    // (the tallies' prefix in one DPP scan; its exchange array is not reused, so the barrier
+    // after the s_pre stores is the only one after it)
+    uint32_t a32 = (uint32_t)(ta0 + ta1), b32 = (uint32_t)(tb0 + tb1), ta32, tb32;
+    block_exclusive_scan2_32<false>(a32, b32, ta32, tb32, s_sh);
+    const long long a = a32, b = b32, tot_a = ta32, tot_b = tb32;
     if (i0 < p.n_pblocks) {
       s_pre[2 * i0] = a;
       s_pre[2 * i0 + 1] = b;
@@ -989,17 +998,12 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
       s_pre[2 * i0 + 2] = a + ta0;
       s_pre[2 * i0 + 3] = b + tb0;
     }
-    if (threadIdx.x == 0) {
-      const unsigned long long d = p.sc->draw;  // (folded by this tick's k_pick)
-      s_base[0] = d;
-      s_base[1] = d + (unsigned long long)tot_a;
-      if (blockIdx.x == 0) {
-        p.sc->draw_pend = (unsigned long long)(tot_a + tot_b);
-        if (targ < 0) drain_decide(p, n_before, max_drain, (-1 - targ) ^ 1);  // the next drain tick
-      }
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+      p.sc->draw_pend = (unsigned long long)(tot_a + tot_b);
+      if (targ < 0) drain_decide(p, n_before, max_drain, (-1 - targ) ^ 1);  // the next drain tick
     }
     __syncthreads();
-    bs = Bases{s_base[0], s_base[1], s_pre};
+    bs = Bases{d0, d0 + (unsigned long long)tot_a, s_pre};
     if (send) sd = bs.send + (unsigned long long)s_pre[2 * (v / kGThreads) + 1] + (unsigned long long)p.lsend[v];
   } else {
     bs = Bases{p.sc->base_trig, p.sc->base_send, p.bsum};
