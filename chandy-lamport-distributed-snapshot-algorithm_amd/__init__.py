@@ -22,7 +22,8 @@ __all__ = ["ChandyLamportSim", "GlobalSnapshot", "MsgSnapshot", "PassTokenEvent"
            "ClSnapError", "lib", "go_delay_schedule", "go_int63", "go_intn", "REFERENCE_SEED",
            "INST_OK", "INST_FATAL_INSUFFICIENT_TOKENS", "INST_FATAL_UNKNOWN_DEST",
            "INST_FIFO_OVERFLOW", "INST_HANG", "INST_DELAY_EXHAUSTED", "COUNTER_NAMES",
-           "SUM_NAMES", "MAX_DELAY"]
+           "SUM_NAMES", "MAX_DELAY", "E_INVALID", "E_UNKNOWN_NODE", "E_DUPLICATE_NODE", "E_PARSE",
+           "E_IO", "E_DEVICE", "E_LIMIT", "E_STATE", "E_NOT_COMPLETE"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libclsnap.so")
@@ -38,8 +39,12 @@ COUNTER_NAMES = ("push", "peek", "pop_tok", "pop_mk", "recorded", "completed", "
 SUM_NAMES = ("instances", "ok", "fatal", "other", "delivered", "snapshot_hash", "cut_residual",
              "final_residual", "completed", "in_flight")
 
-_ERRORS = {-1: "invalid", -2: "unknown node", -3: "duplicate node", -4: "parse", -5: "io",
-           -6: "device", -7: "limit", -8: "state", -9: "not complete"}
+# the C ABI's return codes (include/clsnap.h CL_E_*)
+(E_INVALID, E_UNKNOWN_NODE, E_DUPLICATE_NODE, E_PARSE, E_IO, E_DEVICE, E_LIMIT, E_STATE,
+ E_NOT_COMPLETE) = range(-1, -10, -1)
+_ERRORS = {E_INVALID: "invalid", E_UNKNOWN_NODE: "unknown node", E_DUPLICATE_NODE: "duplicate node",
+           E_PARSE: "parse", E_IO: "io", E_DEVICE: "device", E_LIMIT: "limit", E_STATE: "state",
+           E_NOT_COMPLETE: "not complete"}
 
 
 class ClSnapError(RuntimeError):
@@ -111,6 +116,10 @@ def lib():
         "cl_go_intn": [i64, i32, i64, vp],
         "cl_trace_enable": [vp, i64, i32, i32],
         "cl_trace_read": [vp, i64, vp, i32, vp],
+        "cl_set_exec_engine": [vp, i32],
+        "cl_exec_engine": [vp, vp],
+        "cl_jit_stats": [vp, vp],
+        "cl_lanes_compile_check": [vp, vp, vp, i64],
     }
     for name, args in sig.items():
         if os.environ.get("CLSNAP_VARIANT") and not hasattr(L, name):
@@ -125,6 +134,13 @@ def lib():
 
 # Logger record kinds (include/clsnap.h CL_LOG_*)
 LOG_SENT_TOKEN, LOG_SENT_MARKER, LOG_RECV_TOKEN, LOG_RECV_MARKER, LOG_START, LOG_END = range(6)
+
+
+def jit_stats():
+    """Run-time kernel compilations of this process: (total ms, count)."""
+    ms, n = C.c_double(), C.c_int64()
+    _check(lib().cl_jit_stats(C.byref(ms), C.byref(n)))
+    return ms.value, n.value
 
 
 def format_log(ids, records):
@@ -432,6 +448,24 @@ class ChandyLamportSim:
         v = C.c_int32(0)
         _check(self._L.cl_replay_mapped(self._h, C.byref(v)))
         return bool(v.value)
+
+    # exec kernel choice (include/clsnap.h CL_ENGINE_*): results are identical on either kernel
+    ENGINE_AUTO, ENGINE_NODES, ENGINE_LANES = 0, 1, 2
+
+    def set_exec_engine(self, engine):
+        _check(self._L.cl_set_exec_engine(self._h, int(engine)))
+
+    def exec_engine(self):
+        """The exec kernel the most recent launch used (ENGINE_NODES / ENGINE_LANES; 0 before any)."""
+        return self._i32(self._L.cl_exec_engine)
+
+    def lanes_compile_check(self):
+        """Compile the instance-per-lane kernels for this topology without a device:
+        (compile ms, compiler log); raises ClSnapError when they do not fit or fail to compile."""
+        ms = C.c_double()
+        buf = C.create_string_buffer(16384)
+        _check(self._L.cl_lanes_compile_check(self._h, C.byref(ms), buf, len(buf)))
+        return ms.value, buf.value.decode(errors="replace")
 
     def kernel_time(self):
         """(total exec-kernel ms, launches) since the previous call (HIP events)."""

@@ -209,6 +209,27 @@ struct ColumnC {
                            w_pend = w_trig + (D + 1) / 2;
 };
 
+// ---- instance-per-lane kernel (cl_lanes.h, cl_jit.cpp) ------------------------------
+// Small topologies (N <= 16 nodes, every degree <= 4) can run one instance per lane, with the
+// topology compiled into the kernel: a node's state lives in registers of fixed slots, only
+// the FIFO rings and the delay row live in the lane's LDS column.  The host describes the
+// frozen topology here (the JIT generates the kernel's topology type from it); init_tok is
+// read by the kernel at its start.
+constexpr int32_t kLanesMaxNodes = 16;
+constexpr int32_t kLanesMaxDegree = 4;
+// AUTO picks the instance-per-lane kernel only from this batch size up: one wave per 64
+// instances needs >= 4 waves per SIMD (1024 SIMDs) to hide its issue latency; smaller batches
+// run faster node-parallel (C2, 65,536 instances: 0.31 ms per step on lanes vs 0.153 ms)
+constexpr int64_t kLanesAutoMinInstances = 1 << 18;
+struct LanesTopo {
+  int32_t ok;                       // the topology fits the kernel (set by the host)
+  uint32_t node[kLanesMaxNodes];    // indeg (3..0) | outdeg (7..4) | out_off (15..8)
+  uint32_t inl[kLanesMaxNodes];     // in-link j at bits 8j..8j+7: sender rank (3..0) | its out-index (5..4)
+  int32_t init_tok[kLanesMaxNodes]; // tokens at the start (readTopologyFile)
+  int32_t max_payload;              // largest token count a send of the program moves
+  int32_t max_depth;                // most packets the program can ever push on one channel
+};
+
 // Kernel parameters (passed by value).
 struct ExecParams {
   int32_t op_begin, op_end;
@@ -251,6 +272,8 @@ struct ExecParams {
   const int32_t* ch_dest;   // [C] dest rank of channel c
   int64_t trace_lo;
   int32_t trace_n, trace_cap;
+  // the topology in the form the instance-per-lane kernels are generated from (cl_jit.cpp)
+  LanesTopo lt;
 };
 
 struct SumParams {
@@ -294,6 +317,22 @@ struct ExecLaunch {
   int32_t* stop2_used;
 };
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
+// The instance-per-lane kernel (cl_lanes.h, compiled per topology by cl_jit.cpp): lanes_fit
+// says whether a launch can take it; launch_lanes runs it (same outputs, state image and replay
+// plan as launch_exec; hipErrorInvalidImage when the kernel could not be compiled, lanes_error
+// says why); lanes_jit_stats: run-time compilations so far and their total time.
+bool lanes_fit(const ExecParams& p);
+int launch_lanes(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
+const char* lanes_error();
+void lanes_jit_stats(double* compile_ms, int64_t* compiles);
+}  // namespace clsnap
+#if !defined(__HIPCC_RTC__)
+#include <string>
+namespace clsnap {
+int lanes_compile_only(const ExecParams& p, double* ms, std::string* log);
+}  // namespace clsnap
+#endif
+namespace clsnap {
 int launch_checksums(const SumParams& p, void* stream);
 
 // CollectSnapshot (sim.go:134-173) of snapshot `sid` for instances [lo, lo + n), packed on

@@ -226,6 +226,10 @@ struct cl_sim {
   std::vector<std::vector<int32_t>> hist;  // token history per channel (push order)
   std::vector<int32_t> depth_bound;        // packets ever pushed per channel
 
+  // exec kernel choice (cl_set_exec_engine) and the one the latest launch used
+  int32_t engine = CL_ENGINE_AUTO;
+  int32_t last_engine = 0;
+
   // limits
   int32_t cap_log2 = 3;
   bool auto_cap = true;  // choose cap_log2 per layout (cl_set_limits with slots > 0 pins it)
@@ -532,6 +536,42 @@ struct cl_sim {
     return CL_OK;
   }
 
+  // The layout the next launch would use: s_cap, the LDS ring size and the delay row (no
+  // allocation; ensure_layout applies it).
+  Layout plan_layout(int32_t* s_cap_out, int32_t* cap_log2_out, int64_t* row_out) const {
+    const int n = (int)ids.size();
+    const int32_t want_s = std::max<int32_t>(4, (n_sids + 3) / 4 * 4);
+    const int32_t sc = std::max(want_s, s_cap);
+    const int64_t row = go_seeds ? std::max<int64_t>(16, (draws_needed() + 15) / 16 * 16) : (user_draws + 15) / 16 * 16;
+    const int32_t od = std::max(max_out, 1), id = std::max(max_in, 1);
+    int32_t cl = cap_log2;
+    if (auto_cap) {
+      // LDS ring slots per channel: enough for the deepest channel (spill beyond), but
+      // small enough that LDS does not cap the workgroups per CU below kTargetBlocks.
+      int32_t mx = 1;
+      for (auto d : depth_bound) mx = std::max(mx, d);
+      int l = 1;
+      while (l < 3 && (1 << l) < mx) ++l;  // at most 8 slots
+      for (; l > 1; --l) {
+        Layout t = make_layout(n, od, id, l, -1, sc, row, kDelayStageWords);
+        if ((int64_t)t.wave_words * kWavesPerBlock * 4 * kTargetBlocks <= kMaxLdsBytes) break;
+      }
+      cl = l;
+    }
+    int32_t mx = 0;
+    for (auto d : depth_bound) mx = std::max(mx, d);
+    int ocap = -1;
+    if (mx > (1 << cl)) {
+      int need = std::min(mx, kMaxQueued) - (1 << cl), l = 0;
+      while ((1 << l) < need) ++l;
+      ocap = l;
+    }
+    if (s_cap_out) *s_cap_out = sc;
+    if (cap_log2_out) *cap_log2_out = cl;
+    if (row_out) *row_out = row;
+    return make_layout(n, od, id, cl, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), sc, row, kDelayStageWords);
+  }
+
   // Allocate per-instance state and outputs for the current layout.
   int ensure_layout() {
     const int n = (int)ids.size(), C = (int)ch_dst.size();
@@ -541,27 +581,13 @@ struct cl_sim {
         layout_row == (go_seeds ? std::max<int64_t>(16, (draws_needed() + 15) / 16 * 16) : (user_draws + 15) / 16 * 16))
       return CL_OK;
     if (dev_ready) HIP_TRY(hipStreamSynchronize(stream));  // (buffers below may be reallocated or rewritten)
-    s_cap = std::max(want_s, s_cap);
-    if (s_cap > kMaxSnapshots) return set_err(CL_E_LIMIT, "more than %d snapshots", kMaxSnapshots);
     if (n == 0) return set_err(CL_E_STATE, "the topology has no nodes");
-    const int64_t row = go_seeds ? std::max<int64_t>(16, (draws_needed() + 15) / 16 * 16) : (user_draws + 15) / 16 * 16;
-    const int32_t od = std::max(max_out, 1), id = std::max(max_in, 1);
-    if (auto_cap) {
-      // LDS ring slots per channel: enough for the deepest channel (spill beyond), but
-      // small enough that LDS does not cap the workgroups per CU below kTargetBlocks.
-      int32_t mx = 1;
-      for (auto d : depth_bound) mx = std::max(mx, d);
-      int l = 1;
-      while (l < 3 && (1 << l) < mx) ++l;  // at most 8 slots
-      for (; l > 1; --l) {
-        Layout t = make_layout(n, od, id, l, -1, s_cap, row, kDelayStageWords);
-        if ((int64_t)t.wave_words * kWavesPerBlock * 4 * kTargetBlocks <= kMaxLdsBytes) break;
-      }
-      cap_log2 = l;
-      ocap = ocap_log2_needed();
-    }
-    Layout L = make_layout(n, od, id, cap_log2, std::max(ocap, lay.wave_words ? lay.ocap_log2 : -1), s_cap,
-                           row, kDelayStageWords);
+    int64_t row = 0;
+    int32_t sc = 0, cl = 0;
+    Layout L = plan_layout(&sc, &cl, &row);
+    s_cap = sc;
+    cap_log2 = cl;
+    if (s_cap > kMaxSnapshots) return set_err(CL_E_LIMIT, "more than %d snapshots", kMaxSnapshots);
     if (4ull * s_cap * stride * (uint64_t)n * (uint64_t)L.rw >= (1ull << 32) ||  // byte offsets
         (uint64_t)L.state_words * stride >= (1ull << 32))
       return set_err(CL_E_LIMIT, "batch too large for 32-bit output indexing; split it");
@@ -639,6 +665,28 @@ struct cl_sim {
     dmap[ops.size()] = (int32_t)dops.size();
   }
 
+  // The frozen topology in the form the instance-per-lane kernels are generated from (cl_jit.cpp):
+  // ok only for N <= 16 nodes with every degree <= 4.
+  LanesTopo lanes_topo() const {
+    LanesTopo t{};
+    const int n = (int)ids.size();
+    if (n < 1 || n > kLanesMaxNodes || max_out > kLanesMaxDegree || max_in > kLanesMaxDegree) return t;
+    for (int v = 0; v < n; ++v) {
+      const int id = in_off[v + 1] - in_off[v], od = out_off[v + 1] - out_off[v];
+      t.node[v] = (uint32_t)id | ((uint32_t)od << 4) | ((uint32_t)out_off[v] << 8);
+      for (int j = 0; j < id; ++j) {
+        const int c = in_ch[in_off[v] + j], src = ch_src[c];
+        t.inl[v] |= ((uint32_t)src | ((uint32_t)(c - out_off[src]) << 4)) << (8 * j);
+      }
+      t.init_tok[v] = init_tok[v];
+    }
+    t.ok = out_off[n] <= 255 ? 1 : 0;
+    for (const Op& o : ops)
+      if (o.kind == OP_SEND) t.max_payload = std::max(t.max_payload, o.c);
+    for (auto d : depth_bound) t.max_depth = std::max(t.max_depth, d);
+    return t;
+  }
+
   ExecParams exec_params(int32_t op_begin, int32_t n_started_before) const {
     ExecParams p{};
     const int n = (int)ids.size(), C = (int)ch_dst.size();
@@ -662,6 +710,7 @@ struct cl_sim {
     p.ovf = d_ovf.p;
     p.ovh = d_ovh.p;
     p.ch_dest = d_ch_dest.p;
+    p.lt = lanes_topo();
     if (trace_n > 0) {
       p.trace = d_trace.p;
       p.trace_cnt = d_trace_cnt.p;
@@ -745,10 +794,26 @@ struct cl_sim {
     // step) and bracketed ~1 us of packet processing into the kernel time
     const bool pipe = CLSNAP_PIPE && planned && p.split_slot > 0 && p.split_slot < n_inst && stream2 && !save_state;
     if (!pipe && (rc = join_stream2())) return rc;
-    int e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p,
-                        ExecLaunch{stream, pr.start, pr.stop, stream2, ev_fork, ev_join,
-                                   pipe && CLSNAP_PIPE == 1 ? (s_dirty ? 1 : 0) : 1, pipe ? 0 : 1, pr.stop2,
-                                   &pr.stop2_used});
+    const ExecLaunch el{stream, pr.start, pr.stop, stream2, ev_fork, ev_join,
+                        pipe && CLSNAP_PIPE == 1 ? (s_dirty ? 1 : 0) : 1, pipe ? 0 : 1, pr.stop2, &pr.stop2_used};
+    // the instance-per-lane kernel, compiled for this topology, wherever it fits (N <= 16, every
+    // degree <= 4) and the batch fills the chip with one instance per lane (AUTO); the
+    // node-parallel kernel otherwise, or when run-time compilation failed
+    const bool lanes = engine != CL_ENGINE_NODES && lanes_fit(p) &&
+                       (engine == CL_ENGINE_LANES || (int64_t)n_inst >= kLanesAutoMinInstances);
+    if (engine == CL_ENGINE_LANES && !lanes)
+      return set_err(CL_E_LIMIT, "the instance-per-lane kernel needs <= %d nodes, degrees <= %d, <= 16 snapshots",
+                     kLanesMaxNodes, kLanesMaxDegree);
+    int e = lanes ? launch_lanes(p, d_topo.p, d_ops.p, d_sched.p, el) : launch_exec(p, d_topo.p, d_ops.p, d_sched.p, el);
+    if (lanes && e == (int)hipErrorInvalidImage) {
+      if (engine == CL_ENGINE_LANES)
+        return set_err(CL_E_DEVICE, "instance-per-lane kernel compilation failed: %s", lanes_error());
+      std::fprintf(stderr, "clsnap: instance-per-lane kernel unavailable, using the node-parallel kernel: %s\n",
+                   lanes_error());
+      engine = CL_ENGINE_NODES;
+      e = launch_exec(p, d_topo.p, d_ops.p, d_sched.p, el);
+    }
+    last_engine = lanes && engine != CL_ENGINE_NODES ? CL_ENGINE_LANES : CL_ENGINE_NODES;
     if (pipe) {
       s2_live = true;
       s_dirty = false;
@@ -1318,6 +1383,54 @@ int cl_replay_mapped(cl_sim* sim, int32_t* on) {
 int cl_synchronize(cl_sim* sim) {
   SIM_CHECK(sim);
   return sim->sync();
+}
+
+int cl_set_exec_engine(cl_sim* sim, int32_t engine) {
+  SIM_CHECK(sim);
+  if (engine != CL_ENGINE_AUTO && engine != CL_ENGINE_NODES && engine != CL_ENGINE_LANES)
+    return set_err(CL_E_INVALID, "unknown exec engine %d", engine);
+  if (engine != sim->engine) {
+    // the next launch replays the program from the start on the chosen kernel (results are the
+    // same; the resumable state image is shared by both kernels)
+    sim->engine = engine;
+    sim->plan_ops = sim->plan_tried = -1;
+  }
+  return CL_OK;
+}
+
+int cl_exec_engine(cl_sim* sim, int32_t* engine) {
+  SIM_CHECK(sim);
+  if (!engine) return set_err(CL_E_INVALID, "null output");
+  *engine = sim->last_engine;
+  return CL_OK;
+}
+
+int cl_lanes_compile_check(cl_sim* sim, double* compile_ms, char* log, int64_t log_cap) {
+  SIM_CHECK(sim);
+  int rc = sim->freeze();
+  if (rc) return rc;
+  if (sim->ids.empty()) return set_err(CL_E_STATE, "the topology has no nodes");
+  ExecParams p{};
+  int64_t row = 0;
+  p.lay = sim->plan_layout(nullptr, nullptr, &row);
+  p.n_nodes = (int32_t)sim->ids.size();
+  p.n_ch = (int32_t)sim->ch_dst.size();
+  p.sched_row = row;
+  p.lt = sim->lanes_topo();
+  if (!lanes_fit(p)) return set_err(CL_E_LIMIT, "the topology does not fit the instance-per-lane kernel");
+  std::string l;
+  rc = lanes_compile_only(p, compile_ms, &l);
+  if (log && log_cap > 0) {
+    const size_t n = std::min<size_t>(l.size(), (size_t)log_cap - 1);
+    std::memcpy(log, l.data(), n);
+    log[n] = 0;
+  }
+  return rc ? set_err(CL_E_DEVICE, "instance-per-lane kernel compilation failed") : CL_OK;
+}
+
+int cl_jit_stats(double* compile_ms, int64_t* compiles) {
+  clsnap::lanes_jit_stats(compile_ms, compiles);
+  return CL_OK;
 }
 
 int cl_debug_poison_outputs(cl_sim* sim) {

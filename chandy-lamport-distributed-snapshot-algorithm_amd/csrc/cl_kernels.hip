@@ -581,9 +581,12 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
       const uint32_t sid = tv >> 8;
       // exclusive prefix of the triggering sender within the instance
       const int32_t k0 = ln.draw + (int32_t)(XW(lay.x_off + x.seg_base + src) - (uint32_t)x.outdeg - base);
-      if constexpr (STAGED) {
+      if constexpr (STAGED && hw_reg(D)) {
         // the broadcast's delays, read together (k0 + j may pass the schedule's end only in
-        // an instance that push() then freezes; the staged rows stay inside the wave's LDS)
+        // an instance that push() then freezes; the staged rows stay inside the wave's LDS).
+        // Only where the heads live in registers (hw_reg): push_pred writes channel j's head
+        // back even for j >= outdeg (unchanged), which with LDS heads (D = 8..128) is another
+        // node's channel, possibly another wave's (a lost update when that one pushes too)
         uint32_t dl[D];
 #pragma unroll
         for (int32_t j = 0; j < D; ++j) dl[j] = x.lrow[k0 + j];

@@ -162,6 +162,26 @@ int cl_replay_split(cl_sim* sim, int64_t* spill_instances, int64_t* split_slot);
  * results unchanged). */
 int cl_replay_mapped(cl_sim* sim, int32_t* on);
 
+/* Which exec kernel runs the program (engine-internal; results are identical):
+ *   CL_ENGINE_AUTO   the instance-per-lane kernel, compiled at run time for this topology
+ *                    (hipRTC), wherever the topology fits it (<= 16 nodes, every degree <= 4,
+ *                    <= 16 snapshot ids); else -- or when run-time compilation fails -- the
+ *                    node-parallel kernel
+ *   CL_ENGINE_NODES  the node-parallel kernel (one lane per node)
+ *   CL_ENGINE_LANES  the instance-per-lane kernel; CL_E_LIMIT where the topology does not fit
+ * cl_exec_engine reports the kernel the most recent launch used (0 before any). */
+#define CL_ENGINE_AUTO 0
+#define CL_ENGINE_NODES 1
+#define CL_ENGINE_LANES 2
+int cl_set_exec_engine(cl_sim* sim, int32_t engine);
+int cl_exec_engine(cl_sim* sim, int32_t* engine);
+/* Run-time kernel compilations of this process so far and their total wall time. */
+int cl_jit_stats(double* compile_ms, int64_t* compiles);
+/* Compile the instance-per-lane kernels for this sim's topology and layout without loading
+ * them (no device needed): CL_OK, or CL_E_LIMIT (the topology does not fit them) / CL_E_DEVICE
+ * (compilation failed); the compiler log goes to log (log_cap bytes, may be NULL). */
+int cl_lanes_compile_check(cl_sim* sim, double* compile_ms, char* log, int64_t log_cap);
+
 /* Test/benchmark aid (no reference counterpart): overwrite every result plane the exec
  * kernel writes -- node snapshot records, completion ticks, per-instance result rows,
  * final node tokens -- with the byte 0xA5 on the sim's stream, so that results read after

@@ -13,7 +13,7 @@ import pytest
 
 import oracle as O
 from enginecheck import (batch_sums_from_oracle, canonical, cl, compare_instance, engine_run,
-                         oracle_batch, oracle_run)
+                         new_sim, oracle_batch, oracle_run)
 from snapcheck import TEST_DATA, assert_equal, check_tokens, read_snapshot_file, scenarios
 
 pytestmark = pytest.mark.gpu
@@ -128,7 +128,7 @@ def test_incremental_flush_equals_one_shot():
     lines = open(os.path.join(TEST_DATA, "8nodes-concurrent-snapshots.events")).read().split("\n")
     n = 256
     a = engine_run(top, "8nodes-concurrent-snapshots.events", n)
-    b = cl.ChandyLamportSim(n)
+    b = new_sim(n)
     b.read_topology_file(os.path.join(TEST_DATA, top))
     for line in lines:
         if not line:
@@ -306,10 +306,13 @@ def test_wait_snapshot_after_back_to_back_split_reruns():
         sim.rerun()
         sim.rerun()   # back to back: no join of the second stream in between
         v = ctypes.c_int64(-1)
+        timeout_ms = 20_000
         t0 = time.perf_counter()
-        rc = sim._L.cl_wait_snapshot(sim._h, sid, 0, n, 20_000, ctypes.byref(v))
+        rc = sim._L.cl_wait_snapshot(sim._h, sid, 0, n, timeout_ms, ctypes.byref(v))
         waited = time.perf_counter() - t0
-        assert rc == -9 and v.value == want[sid] and waited < 10.0, (sid, rc, v.value, want[sid], waited)
+        # returning at once, not after the timeout (half of it: room for a slow box)
+        assert rc == cl.E_NOT_COMPLETE and v.value == want[sid] and waited < timeout_ms / 2000, \
+            (sid, rc, v.value, want[sid], waited)
         sim.rerun()
         assert sim.poll_snapshot(sid) == want[sid]
 
@@ -326,7 +329,7 @@ def test_replay_plan_spill_free_and_split():
     top = "3\nA 10\nB 10\nC 10\nA B\nB C\nC A\nB A\n"
     ev = "send A B 2\ntick 6\nsnapshot A\ntick 6\nsnapshot B\n"
     n = 512
-    sim = cl.ChandyLamportSim(n, fifo_lds_slots=2)
+    sim = new_sim(n, fifo_lds_slots=2)
     sim.read_topology_text(top)
     sim.read_events_text(ev)
     sim.flush()
@@ -346,7 +349,7 @@ def test_replay_plan_spill_free_and_split():
     sim.rerun()                   # the new program's probe: every instance spills, no split
     sim.synchronize()
     assert sim.replay_split() == (n, 0)
-    ref = cl.ChandyLamportSim(n, fifo_lds_slots=2)  # the same two readEventsFile calls, one flush
+    ref = new_sim(n, fifo_lds_slots=2)  # the same two readEventsFile calls, one flush
     ref.read_topology_text(top)
     ref.read_events_text(ev)
     ref.read_events_text(ev2)
@@ -405,7 +408,7 @@ def test_headline_batch_fresh_path_matches_fixture():
     fx = json.load(open(os.path.join(os.path.dirname(TEST_DATA), "bench_sums.json")))
     want = fx["batches"]["c3"]["sums"]
     n = fx["batches"]["c3"]["instances"]
-    sim = cl.ChandyLamportSim(n, seed_base=O.REFERENCE_SEED)
+    sim = new_sim(n, seed_base=O.REFERENCE_SEED)
     sim.read_topology_file(os.path.join(TEST_DATA, "8nodes.top"))
     sim.read_events_file(os.path.join(TEST_DATA, "8nodes-concurrent-snapshots.events"))
     sim.rerun()                    # the first launch: nothing derived from a prior run
@@ -430,7 +433,7 @@ def test_two_event_texts_and_snapshot_after_drain():
     ev1 = "send A B 3\nsnapshot A\ntick 2\nsend C D 1\n"
     ev2 = "snapshot C\nsend B A 2\ntick 3\nsnapshot D\n"
     n = 128
-    sim = cl.ChandyLamportSim(n)
+    sim = new_sim(n)
     sim.read_topology_text(top)
     sim.read_events_text(ev1)
     sim.flush()
@@ -505,3 +508,26 @@ def test_packed_collect_equals_host_expansion_and_oracle():
         assert np.array_equal(rm, m2)
     assert total == sim.counters(only_ok=False)["recorded"]
     assert sim.collect_time() > 0
+
+
+def test_uneven_fan_out_runtime_loop_kernel():
+    """a hub with 10 out-links (degree bound 16: the run-time-loop kernel with its
+    heads in LDS) next to leaves of in-degree <= 2 -- marker broadcasts at the hub must touch
+    only its own channels' heads.  1-4 overlapping snapshots, sends from the hub."""
+    leaves = [f"L{k}" for k in range(10)]
+    top = f"{len(leaves) + 1}\nH 40\n" + "".join(f"{x} 5\n" for x in leaves)
+    top += "".join(f"H {x}\n" for x in leaves)
+    top += "".join(f"{leaves[k]} {leaves[(k + 1) % 10]}\n" for k in range(10)) + "L0 H\n"
+    for n_snap in (1, 2, 4):
+        ev = []
+        for r in range(n_snap):
+            ev += [f"send H {leaves[(3 * r) % 10]} 2", f"snapshot {'H' if r % 2 == 0 else leaves[r]}",
+                   f"send L{r} L{r + 1} 1", "tick 2"]
+        events = "\n".join(ev) + "\n"
+        n = 512
+        sim = engine_run(top, events, n)
+        status, times = sim.status(), sim.time()
+        assert (status == cl.INST_OK).all()
+        for i in range(n):
+            compare_instance(sim, i, oracle_run(top, events, seed=O.REFERENCE_SEED + i),
+                             status=status, times=times)

@@ -17,6 +17,7 @@ def summary(paths, kernel="cl_exec_kernel"):
 
 if __name__ == "__main__":
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    s = summary(glob.glob(f"{root}/*/p_counter_collection.csv"))
+    kern = sys.argv[2] if len(sys.argv) > 2 else "cl_exec_kernel"
+    s = summary(glob.glob(f"{root}/*/p_counter_collection.csv"), kern)
     for k in sorted(s):
         print(f"{k:28s} {s[k]:16.1f}")
