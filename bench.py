@@ -272,6 +272,7 @@ def main(argv=None):
     sums = sim.checksums()
     recorded_ok = sim.counters(only_ok=True)["recorded"]
     collect = collect_all(sim, args) if not args.no_collect else None
+    engine = sim.exec_engine()
     spilled, split = sim.replay_split()
     replay = {"slot_map": sim.mapped_replays(), "spill_free": sim.spill_free_replays(),
               "spilled_instances": spilled, "split_slot": split}
@@ -370,7 +371,10 @@ def main(argv=None):
                                         "concurrently (section 5), both inside kernel_ms"),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": hbm_frac,
-                         "traffic": traffic, "kernel": "cl_exec_kernel",
+                         "traffic": traffic,
+                         "kernel": ("clsnap_lanes_nospill (instance per lane, hipRTC-specialized to the "
+                                    "topology)" + (" + cl_exec_kernel on the spilling instances" if split else "")
+                                    if engine == cl.ChandyLamportSim.ENGINE_LANES else "cl_exec_kernel"),
                          "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg,
                          "scope": f"whole node: {world} GPU(s), bytes summed over ranks, slowest rank's "
                                   f"average kernel time, peak {world} x {HBM_PEAK_GBS:g} GB/s",

@@ -585,8 +585,9 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
         // the broadcast's delays, read together (k0 + j may pass the schedule's end only in
         // an instance that push() then freezes; the staged rows stay inside the wave's LDS).
         // Only where the heads live in registers (hw_reg): push_pred writes channel j's head
-        // back even for j >= outdeg (unchanged), which with LDS heads (D = 8..128) is another
-        // node's channel, possibly another wave's (a lost update when that one pushes too)
+        // back even for j >= outdeg (unchanged), which with LDS heads (D = 8..128) lands past
+        // the lane's out-links -- for j >= priv - w_lnk past its column, in the next wave's
+        // region (tests/test_gpu_parity.py::test_uneven_fan_out_runtime_loop_kernel)
         uint32_t dl[D];
 #pragma unroll
         for (int32_t j = 0; j < D; ++j) dl[j] = x.lrow[k0 + j];
