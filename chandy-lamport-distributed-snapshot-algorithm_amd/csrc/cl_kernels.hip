@@ -454,8 +454,10 @@ __device__ __forceinline__ void refill(const Ctx& x, int32_t ko, uint32_t slot) 
 // Tick (sim.go:71-95) for every lane whose instance is `act` (uniform per segment).
 // Must be reached by all lanes of the wave.  D bounds every node's in/out degree;
 // it[] holds this node's in-link words.
+// Returns true when no lane of the wave picked a packet: the tick ended after phase A (B, C
+// and D would change nothing; phase A counted the peeks).
 template <int D, bool STAGED, bool TRACE, bool NOSPILL = false>
-__device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act) {
+__device__ __forceinline__ bool tick(const Ctx& x, Lane& ln, const InLinks<D>& it, bool act) {
   const Layout& lay = x.lay;
   const uint32_t cap = 1u << lay.cap_log2;
   const unsigned long long pt0 = PROF_T();
@@ -512,6 +514,10 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
   if constexpr (!(unrolled(D) && CLSNAP_B_PRED)) {
     XW(lay.x_pick + x.lane) = pick;
     wave_sync();
+  }
+  if (!__ballot(pick != 0)) {
+    PROF_ADD(ln, 2, pt0);
+    return true;
   }
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
@@ -617,6 +623,7 @@ __device__ __forceinline__ void tick(const Ctx& x, Lane& ln, const InLinks<D>& i
 #if CLSNAP_PROF
   ln.prof[7] += 1;
 #endif
+  return false;
 }
 
 // SendTokens (node.go:112-131) of one send event: balance check, link lookup, push -- all
@@ -896,7 +903,24 @@ __device__ __forceinline__ void exec_wave(const ExecParams& p, const Layout& lay
         }
         const bool act = ln.alive && iter < until;
         if (!__ballot(act)) break;
-        tick<D, STAGED, TRACE, (CAP > 0 && !SPILL)>(x, ln, it, act);
+        const bool idle = tick<D, STAGED, TRACE, (CAP > 0 && !SPILL)>(x, ln, it, act);
+        if (idle && !anyw) {
+          // nothing picked, and if nothing is queued anywhere in the wave either, every
+          // remaining tick of this op is empty for every lane (no peek, draw or delivery: the
+          // drain tail after the last delivery) -- add them at once
+          uint32_t q = 0;
+          if constexpr (hw_reg(D)) {
+#pragma unroll
+            for (int32_t k = 0; k < D; ++k)
+              if (k < outdeg) q |= hw_get<D>(x, ln, k) >> 8;
+          } else {
+            for (int32_t k = 0; k < outdeg; ++k) q |= CHW(k) >> 8;
+          }
+          if (!__ballot(q != 0)) {
+            if (ln.alive) ln.time += max(0, until - (iter + 1));
+            break;
+          }
+        }
       }
 #if CLSNAP_PROF
       PROF_ADD(ln, 4, ot0);

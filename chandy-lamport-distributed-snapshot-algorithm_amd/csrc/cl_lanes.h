@@ -284,9 +284,19 @@ __device__ __forceinline__ void resolve(State<T>& s) {
   s.flag = 0;
 }
 
+// Code-shape knobs (A/B through cl_jit.cpp CLSNAP_LANES_DEFS)
+#ifndef LANES_EARLY
+#define LANES_EARLY 1  // end the tick after phase A when no lane of the wave picked a packet
+#endif
+
+#ifndef LANES_TAIL
+#define LANES_TAIL 1  // after such a tick with nothing queued anywhere, skip the op's remaining ticks
+#endif
+
 // Tick (sim.go:71-95) for a lane whose instance is `act`.  Every lane of the wave calls it.
+// Returns true when no lane of the wave picked a packet (the tick ended after phase A).
 template <class T, bool SPILL>
-__device__ __forceinline__ void tick(const Ctx& x, State<T>& s, bool act) {
+__device__ __forceinline__ bool tick(const Ctx& x, State<T>& s, bool act) {
   constexpr int N = T::N, D = T::D;
   s.time += act ? 1 : 0;
   // ---- A: pick ------------------------------------------------------------------------
@@ -336,6 +346,17 @@ __device__ __forceinline__ void tick(const Ctx& x, State<T>& s, bool act) {
     }
     sched_fence();
   }
+#if LANES_EARLY
+  // nothing due anywhere in the wave (15 % of C3's wave-ticks, mostly drain tails): the tick
+  // ends here -- phase A already counted its peeks, and B, the completion check and C/D
+  // would change nothing
+  {
+    uint32_t any = 0;
+#pragma unroll
+    for (int v = 0; v < N; ++v) any |= pk[v];
+    if (!__ballot(any != 0)) return true;
+  }
+#endif
   // ---- B: receive, in-links in ascending sender rank ----------------------------------------
   // Straight-line and predicated: every register update happens on every lane (selects), only
   // the two snapshot-record stores sit in (divergent) branches -- register writes inside a
@@ -474,6 +495,7 @@ __device__ __forceinline__ void tick(const Ctx& x, State<T>& s, bool act) {
     s.draw += (int32_t)acc;
   }
   resolve(s);
+  return false;
 }
 
 // Host ops name their node (and link) by uniform indices.  They are straight-line: the node's
@@ -749,7 +771,22 @@ __device__ __forceinline__ void program(const ExecParams& p, const Op* __restric
         }
         const bool act = s.alive && iter < until;
         if (!__ballot(act)) break;
-        tick<T, SPILL>(x, s, act);
+        const bool idle = tick<T, SPILL>(x, s, act);
+        if (LANES_TAIL && idle && !anyw) {
+          // no lane picked anything: if nothing is queued anywhere in the wave either, every
+          // remaining tick of this op is empty for every lane (no peek, draw or delivery; the
+          // drain tail after the last delivery, all of C3's idle wave-ticks) -- add them at once
+          uint32_t q = 0;
+#pragma unroll
+          for (int v = 0; v < N; ++v)
+#pragma unroll
+            for (int k = 0; k < D; ++k)
+              if (k < T::od(v)) q |= s.hw[v][k] & 0x7fu;
+          if (!__ballot(q != 0)) {
+            if (s.alive) s.time += max(0, until - (iter + 1));
+            break;
+          }
+        }
       }
     }
   }
