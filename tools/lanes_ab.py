@@ -1,6 +1,6 @@
 """A/B timing of the instance-per-lane kernel on a headline batch: per variant (a value of
 CLSNAP_LANES_DEFS, set by the caller), kernel ms per replay and the checksums against the
-node-parallel engine's.  usage: python tools/lanes_ab.py [c3|c2] [reruns]"""
+node-parallel engine's.  usage: python tools/lanes_ab.py [c3|c2] [reruns] [lanes|nodes|auto]"""
 import importlib, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 m = importlib.import_module("chandy-lamport-distributed-snapshot-algorithm_amd")
@@ -9,9 +9,11 @@ cfgs = {"c3": ("8nodes.top", "8nodes-concurrent-snapshots.events", 1 << 20),
         "c2": ("10nodes.top", "10nodes.events", 65536)}
 name = sys.argv[1] if len(sys.argv) > 1 else "c3"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+eng = {"lanes": m.ChandyLamportSim.ENGINE_LANES, "nodes": m.ChandyLamportSim.ENGINE_NODES,
+       "auto": m.ChandyLamportSim.ENGINE_AUTO}[sys.argv[3] if len(sys.argv) > 3 else "lanes"]
 top, ev, n = cfgs[name]
 s = m.ChandyLamportSim(n_instances=n)
-s.set_exec_engine(m.ChandyLamportSim.ENGINE_LANES)
+s.set_exec_engine(eng)
 s.read_topology_file(G + top)
 s.read_events_file(G + ev)
 s.flush()
@@ -23,5 +25,5 @@ for _ in range(reps):
     s.rerun()
 s.synchronize()
 tot, k = s.kernel_time()
-print(f"{name} defs={os.environ.get('CLSNAP_LANES_DEFS', '')!r} rerun_ms={tot / k:.4f} "
+print(f"{name} engine={s.exec_engine()} variant={os.environ.get('CLSNAP_VARIANT', '')} defs={os.environ.get('CLSNAP_LANES_DEFS', '')!r} rerun_ms={tot / k:.4f} "
       f"sums={s.checksums().tolist()}", flush=True)

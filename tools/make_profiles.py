@@ -17,14 +17,20 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "cl_exec_kernel"
+# the exec kernels: node-parallel, and the instance-per-lane kernels compiled at run time
+KERNELS = ("cl_exec_kernel", "clsnap_lanes")
+KERNEL = " + ".join(KERNELS)
+
+
+def is_exec(name):
+    return any(k in name for k in KERNELS)
 
 
 def per_dispatch(paths):
     vals = collections.defaultdict(dict)  # counter -> dispatch -> value
     for p in paths:
         for r in csv.DictReader(open(p)):
-            if KERNEL not in r["Kernel_Name"]:
+            if not is_exec(r["Kernel_Name"]):
                 continue
             d = int(r["Dispatch_Id"])
             vals[r["Counter_Name"]][d] = vals[r["Counter_Name"]].get(d, 0.0) + float(r["Counter_Value"])
@@ -63,7 +69,7 @@ def main():
                        "hbm_bytes_per_launch": hbm, "fetch_kb": summary["FETCH_SIZE"],
                        "write_kb": summary["WRITE_SIZE"], "round": rnd}, f, indent=1)
     for row in csv.DictReader(open(stats)):
-        if KERNEL in row["Name"]:
+        if is_exec(row["Name"]):
             print(cfg, "avg kernel ns", row["AverageNs"], "calls", row["Calls"])
     print(json.dumps({k: round(v) for k, v in sorted(summary.items())}))
 
