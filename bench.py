@@ -315,7 +315,7 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(top, events, total, args.cpu_baseline_seconds)
 
-    traffic, valu = None, None
+    traffic, valu, traffic_detail = None, None, None
     prof = profile_entry(args.config, per_rank)
     if prof is not None and args.fifo_slots == 0:
         path, d, scale = prof
@@ -323,8 +323,16 @@ def main(argv=None):
         src = os.path.relpath(path, ROOT) + ("" if scale == 1 else
                                              f" (x{scale:g}: per-GPU batch {per_rank} vs profiled {d['instances']})")
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            # whole node, per launch: every rank moves its share
-            traffic = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 * scale * world
+            # whole node, per launch: every rank moves its share.  The exec kernels' reads are
+            # scattered per-instance delay rows, not wide coalesced streams, so the raw count is
+            # the HBM traffic (the guide's 2x FETCH factor would overstate it: C3's raw FETCH_SIZE
+            # equals the 117 MB schedule); the corrected figure rides along (tools/traffic_model.py)
+            traffic = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 * scale * world
+            traffic_detail = {"raw": traffic, "fetch_doubled": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 * scale * world,
+                              "write": c["WRITE_SIZE"] * 1024 * scale * world, "used": "raw",
+                              "why": "the exec kernels read per-instance delay rows scattered by the slot map, "
+                                     "not wide coalesced streams (the guide's 2x FETCH factor applies to those)",
+                              "source": src}
         if "SQ_INSTS_VALU" in c:
             rate = c["SQ_INSTS_VALU"] * scale * world / (avg_kernel_ms * 1e-3)
             valu = {"achieved": rate, "peak": VALU_PEAK * world, "unit": "wave64 VALU instr/s",
@@ -371,7 +379,7 @@ def main(argv=None):
                                         "concurrently (section 5), both inside kernel_ms"),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                          "frac": hbm_frac,
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_detail": traffic_detail,
                          "kernel": ("clsnap_lanes_nospill (instance per lane, hipRTC-specialized to the "
                                     "topology)" + (" + cl_exec_kernel on the spilling instances" if split else "")
                                     if engine == cl.ChandyLamportSim.ENGINE_LANES else "cl_exec_kernel"),
@@ -517,13 +525,16 @@ def bench_graph(args, rank, world, local_rank):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_graph(g, cfg, n, steps, snap_steps, snap_nodes, rs, args.cpu_baseline_seconds)
 
-    traffic = None
+    traffic, traffic_detail = None, None
     tr_path = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tr_path):
         with open(tr_path) as f:
             tr = json.load(f)
         if tr.get("nodes") == n and tr.get("steps") == steps and tr.get("drain", False) == bool(cfg.get("drain")):
-            traffic = tr.get("hbm_bytes_per_launch")
+            traffic = tr.get("hbm_bytes_per_launch")  # raw per kernel unless its reads stream
+            traffic_detail = {k: tr.get(k) for k in ("raw_bytes_per_launch", "corrected_bytes_per_launch")}
+            traffic_detail["used"] = "per kernel: raw, or fetch-doubled where the reads are wide coalesced streams"
+            traffic_detail["source"] = os.path.relpath(tr_path, ROOT)
 
     if rank == 0:
         line = {
@@ -555,7 +566,7 @@ def bench_graph(args, rank, world, local_rank):
             "checks": {"completed": tot["completed"], "cut_residual": tot["cut_residual"],
                        "final_residual": tot["final_residual"], "digest": tot["digest"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_detail": traffic_detail,
                          "kernel": "graph tick pipeline (k_hostops, k_pick, k_marker, k_scan, k_push)",
                          "kernel_ms": avg_run_ms, "alg_bytes_per_launch": alg},
             "cpu_baseline": cpu,

@@ -1475,10 +1475,7 @@ void launch_push(const GParams& p, int32_t t, hipStream_t s) { launch_push(p, t,
 // Small whole-graph runs fold the scan into k_push (C5: 391 node blocks; one launch and its
 // boundary less per tick); large ones keep k_scan (C4: 4,096 tallies per block would be
 // 64 KB of L2 reads per k_push block).
-#ifndef CLSNAP_FUSE_SCAN
-#define CLSNAP_FUSE_SCAN 1
-#endif
-static bool fuse_scan(const GParams& p) { return CLSNAP_FUSE_SCAN && !p.part && p.n_pblocks <= kFuseBlocks; }
+static bool fuse_scan(const GParams& p) { return !p.part && p.n_pblocks <= kFuseBlocks; }
 
 // k_scan on a per-tick latency path: up to 512 block tallies (C5: 391) are scanned by one
 // wave, eight per thread; more by whole waves of four per thread, at most 1024 threads

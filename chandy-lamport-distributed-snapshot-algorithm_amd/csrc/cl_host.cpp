@@ -56,15 +56,9 @@ constexpr int32_t kTargetBlocks = 6;
 // thousand waves: the grouping pays for its one host sort and 4 B per instance of HBM).
 constexpr int64_t kMapMinInstances = 4096;
 
-#ifndef CLSNAP_PIPE
-#define CLSNAP_PIPE 2  // split replays back to back: 0 join every replay, 1 neither fork nor join, 2 fork only (A/B knob)
-#endif
-#ifndef CLSNAP_MAP_PCT
-#define CLSNAP_MAP_PCT 92  // length-ordered slot map when it keeps at most this % of the wave-ticks (A/B knob)
-#endif
-#ifndef CLSNAP_LPT
-#define CLSNAP_LPT 1  // slot map order: 1 longest instances first, 0 shortest first (A/B knob)
-#endif
+// A length-ordered slot map is used when it keeps at most this % of the wave-ticks of the
+// unordered launch (C3 90 %: kept; C2 95 %: measured slower mapped, §9)
+constexpr int64_t kMapPct = 92;
 
 namespace {
 
@@ -327,7 +321,7 @@ struct cl_sim {
   int64_t plan_split = 0, plan_spilled = 0;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  // Split replays back to back (CLSNAP_PIPE): the spill-capable half of a replay on stream2
+  // Split replays back to back: the spill-capable half of a replay on stream2
   // and the spill-free half on `stream` touch disjoint instances, so consecutive replays need
   // no cross-stream wait between them -- a replay's halves overlap the previous replay's
   // tail.  s2_live: stream2 may hold work `stream` has not waited for; every other ABI call
@@ -792,10 +786,12 @@ struct cl_sim {
     // the dispatch records both events (the kernel's own start/end timestamps): two
     // hipEventRecord packets around it cost 0.7 us more per launch (C2 0.1816 -> 0.1809 ms per
     // step) and bracketed ~1 us of packet processing into the kernel time
-    const bool pipe = CLSNAP_PIPE && planned && p.split_slot > 0 && p.split_slot < n_inst && stream2 && !save_state;
+    // split replays back to back fork stream2 from `stream` but do not join it (r03 A/B: joining
+    // every replay, or neither forking nor joining, measured slower)
+    const bool pipe = planned && p.split_slot > 0 && p.split_slot < n_inst && stream2 && !save_state;
     if (!pipe && (rc = join_stream2())) return rc;
-    const ExecLaunch el{stream, pr.start, pr.stop, stream2, ev_fork, ev_join,
-                        pipe && CLSNAP_PIPE == 1 ? (s_dirty ? 1 : 0) : 1, pipe ? 0 : 1, pr.stop2, &pr.stop2_used};
+    const ExecLaunch el{stream, pr.start, pr.stop, stream2, ev_fork, ev_join, 1, pipe ? 0 : 1, pr.stop2,
+                        &pr.stop2_used};
     // the instance-per-lane kernel, compiled for this topology, wherever it fits (N <= 16, every
     // degree <= 4) and the batch fills the chip with one instance per lane (AUTO); the
     // node-parallel kernel otherwise, or when run-time compilation failed
@@ -895,7 +891,7 @@ struct cl_sim {
     for (int32_t i : clean) by_len[(size_t)start[(size_t)std::max(t[(size_t)i], 0)]++] = i;
     // longest waves first (LPT): the dispatcher starts workgroups in slot order as resident
     // ones retire, so the last to start are the shortest and the grid drains evenly
-    if (CLSNAP_LPT) std::reverse(by_len.begin(), by_len.end());
+    std::reverse(by_len.begin(), by_len.end());
     // worth it only when it removes enough wave-ticks to pay for the scattered stores (C3:
     // 43.9 -> 39.5 ticks per wave, kept; C2: 55.8 -> 52.8, measured slower mapped)
     const int64_t nc = (int64_t)clean.size();
@@ -906,7 +902,7 @@ struct cl_sim {
     // a split launches through the map anyway (its scattered result stores are paid), so the
     // clean instances then go in length order too (C2: 0.1829 -> 0.1807 ms per step)
     const bool sort = n_inst >= kMapMinInstances &&
-                      (split || wave_ticks(t, by_len, 0, nc) * 100 <= wave_ticks(t, clean, 0, nc) * CLSNAP_MAP_PCT);
+                      (split || wave_ticks(t, by_len, 0, nc) * 100 <= wave_ticks(t, clean, 0, nc) * kMapPct);
     std::vector<int32_t> order = sort ? by_len : clean;
     order.insert(order.end(), spilled.begin(), spilled.end());
     if (split) plan_split = nc / ipw * ipw;

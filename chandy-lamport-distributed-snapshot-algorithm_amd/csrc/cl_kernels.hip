@@ -144,16 +144,8 @@ struct Lane {
 // Small degree bounds keep loops unrolled and predicated with the in-link words in
 // registers; larger ones use compact runtime loops over the node's own degree with the
 // in-link words in the lane's LDS column (fewer VGPRs, one copy of the marker path).
-// Code-shape knobs (A/B-tested per degree bound):
-//   CLSNAP_UNROLL_MAX  largest D whose loops are unrolled with in-link words in registers
-//   CLSNAP_A_PRED      phase A (pick) as predicated straight-line code (1) or branches (0)
-//   CLSNAP_B_PRED      phase B (receive) likewise
-#ifndef CLSNAP_A_PRED
-#define CLSNAP_A_PRED 1
-#endif
-#ifndef CLSNAP_B_PRED
-#define CLSNAP_B_PRED 1
-#endif
+// CLSNAP_UNROLL_MAX (cl_engine.h) is the largest D whose loops are unrolled; the unrolled
+// phases A and B are predicated straight-line code (branchy forms measured slower, §9).
 #ifndef CLSNAP_MAX_D
 #define CLSNAP_MAX_D 128
 #endif
@@ -170,17 +162,14 @@ __device__ __forceinline__ uint32_t in_key(uint32_t w) {
   return (w & 0xffu) | ((w & 0x7f00u) << 8) | 0x40000000u;
 }
 // In-link recording cursors (delivered-token counts) of the unrolled kernels live in two
-// packed registers instead of the link words' hi16 halves (A/B knob): phase B's per-in-link
-// LDS read + write becomes one add.  The LDS halves are refreshed only for the state image.
-#ifndef CLSNAP_CURREG
-#define CLSNAP_CURREG 1
-#endif
+// packed registers instead of the link words' hi16 halves: phase B's per-in-link LDS read +
+// write becomes one add (r03 A/B, §9).  The LDS halves are refreshed only for the state image.
 // Out-link head words (8-bit ring head, 8-bit count) of the unrolled kernels live in two
 // packed registers instead of the link words' lo16 halves: phase A's and the pushes' LDS
 // reads + writes become register ops; the halves are refreshed for the epilogue (r04 A/B,
 // gpurun_out/r04a: C3 2.380 -> 2.353 ms per step, C2 0.180 -> 0.176 ms).
 constexpr bool hw_reg(int D) { return D <= 4 && CLSNAP_UNROLL_MAX >= D; }
-constexpr bool cur_reg(int D) { return CLSNAP_CURREG && D <= 4 && unrolled(D); }
+constexpr bool cur_reg(int D) { return D <= 4 && unrolled(D); }
 
 #define PW(k) (x.P[(uint32_t)(k) << 6])
 #define XW(k) (x.X[(uint32_t)(k)])
@@ -464,7 +453,7 @@ __device__ __forceinline__ bool tick(const Ctx& x, Lane& ln, const InLinks<D>& i
   ln.time += act ? 1 : 0;
   // ---- A: pick ------------------------------------------------------------
   uint32_t pick = 0, empty_scanned = 0;
-  if constexpr (unrolled(D) && CLSNAP_A_PRED) {
+  if constexpr (unrolled(D)) {
     bool scanning = act;
 #pragma unroll
     for (int32_t ko = 0; ko < D; ++ko) {
@@ -511,7 +500,7 @@ __device__ __forceinline__ bool tick(const Ctx& x, Lane& ln, const InLinks<D>& i
   }
   // the unrolled receive phase reads pick words from the senders' lanes (ds_bpermute); the
   // runtime-loop one, under divergent control flow, from the shared region
-  if constexpr (!(unrolled(D) && CLSNAP_B_PRED)) {
+  if constexpr (!unrolled(D)) {
     XW(lay.x_pick + x.lane) = pick;
     wave_sync();
   }
@@ -521,7 +510,7 @@ __device__ __forceinline__ bool tick(const Ctx& x, Lane& ln, const InLinks<D>& i
   }
   // ---- B: receive, in ascending sender rank ---------------------------------
   int32_t ntrig = 0;
-  if constexpr (unrolled(D) && CLSNAP_B_PRED) {
+  if constexpr (unrolled(D)) {
     // the senders' pick words, read from their lanes (ds_bpermute: no LDS store, no wave
     // sync, no LDS alias that would pin the reads behind the marker path's stores), all
     // issued before the first is used: one LDS round trip per tick, not one per in-link
@@ -706,31 +695,10 @@ __device__ __forceinline__ void send_group(const Ctx& x, Lane& ln, const Op* __r
   if (ln.alive) ln.draw += k;
 }
 
-// Occupancy target per degree bound (waves per SIMD; 256-thread workgroups).  Forcing
-// 8 waves/SIMD at D = 1 costs scratch spills; CLSNAP_OCC selects the policy (0 = let the
-// compiler choose, 1 = force the targets) -- an A/B knob, see DESIGN.md §9.
-#ifndef CLSNAP_W1
-#define CLSNAP_W1 0  // waves/SIMD target for D = 1 (0 = compiler's choice)
-#endif
-#ifndef CLSNAP_W2
-#define CLSNAP_W2 0
-#endif
-#ifndef CLSNAP_W4
-#define CLSNAP_W4 5  // D = 3, 4 with HBM spill rings: 5 waves/SIMD, DESIGN.md §9
-#endif
-#ifndef CLSNAP_SPLIT
-#define CLSNAP_SPLIT 1  // A/B knob: 0 replays a batch with spilling instances wholly on the spill-capable kernel
-#endif
-#ifndef CLSNAP_SPILL_FIRST
-#define CLSNAP_SPILL_FIRST 1  // split replays: dispatch the spill-capable (longest) instances first
-#endif
-#ifndef CLSNAP_W4NS
-#define CLSNAP_W4NS 6  // D = 3, 4 spill-free (the main pass of BASELINE config 3): 6 waves/SIMD
-#endif
-constexpr int waves_for(int D, bool spill) {
-  return D == 1 ? (CLSNAP_W1 ? CLSNAP_W1 : 1) : D == 2 ? (CLSNAP_W2 ? CLSNAP_W2 : 1)
-         : (D == 3 || D == 4) ? (spill ? (CLSNAP_W4 ? CLSNAP_W4 : 1) : CLSNAP_W4NS) : 1;
-}
+// Occupancy target per degree bound (minimum waves per SIMD in the launch bound; 256-thread
+// workgroups), the measured choices of §9: D = 3, 4 at 5 waves with HBM spill rings and 6
+// without (6 and 7 with spill rings cost scratch spills); the others the compiler's choice.
+constexpr int waves_for(int D, bool spill) { return (D == 3 || D == 4) ? (spill ? 5 : 6) : 1; }
 
 // The whole event program for the instances of one wave (slots wave * ipw .. + ipw - 1 of
 // the launch; n_slots slots in all).  Every lane of the wave must call it.
@@ -1294,18 +1262,12 @@ int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, 
   ExecLaunch lb = L;
   lb.ev_stop = L.ev_stop2;
   int e;
-  if (CLSNAP_SPILL_FIRST) {
-    // the spilling instances are the longest: their kernel is dispatched first so its
-    // workgroups are resident from the start instead of queueing behind the main grid (the
-    // tail of a small per-GPU batch); it records the start event
-    if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
-    la.ev_start = nullptr;
-    if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
-  } else {
-    if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
-    lb.ev_start = nullptr;
-    if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
-  }
+  // the spilling instances are the longest: their kernel is dispatched first so its
+  // workgroups are resident from the start instead of queueing behind the main grid (the
+  // tail of a small per-GPU batch); it records the start event
+  if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
+  la.ev_start = nullptr;
+  if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
   if (L.stop2_used && L.ev_stop2) *L.stop2_used = 1;
   if (!L.join) {  // replays back to back: the main stream does not wait for stream2 (cl_host.cpp)
     if (L.ev_stop && (he = hipEventRecord((hipEvent_t)L.ev_stop, s))) return (int)he;
@@ -1330,7 +1292,7 @@ int launch_exec_d(const ExecParams& p, const uint32_t* topo, const Op* ops, cons
       // program never spills (p.nospill) or splits the batch (p.split_slot)
       const bool rings = p.lay.ocap_log2 >= 0 && !p.nospill;
       const bool mp = p.inst_map != nullptr;
-      const bool split = CLSNAP_SPLIT && rings && mp && p.split_slot > 0 && p.split_slot < p.n_inst && L.stream2;
+      const bool split = rings && mp && p.split_slot > 0 && p.split_slot < p.n_inst && L.stream2;
 #define CLSNAP_SPEC(C)                                                                              \
   case C:                                                                                           \
     if (split) return launch_exec_split<D, C>(p, topo, ops, sched, L);                          \

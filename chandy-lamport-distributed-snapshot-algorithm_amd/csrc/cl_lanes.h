@@ -284,15 +284,6 @@ __device__ __forceinline__ void resolve(State<T>& s) {
   s.flag = 0;
 }
 
-// Code-shape knobs (A/B through cl_jit.cpp CLSNAP_LANES_DEFS)
-#ifndef LANES_EARLY
-#define LANES_EARLY 1  // end the tick after phase A when no lane of the wave picked a packet
-#endif
-
-#ifndef LANES_TAIL
-#define LANES_TAIL 1  // after such a tick with nothing queued anywhere, skip the op's remaining ticks
-#endif
-
 // Tick (sim.go:71-95) for a lane whose instance is `act`.  Every lane of the wave calls it.
 // Returns true when no lane of the wave picked a packet (the tick ended after phase A).
 template <class T, bool SPILL>
@@ -346,7 +337,6 @@ __device__ __forceinline__ bool tick(const Ctx& x, State<T>& s, bool act) {
     }
     sched_fence();
   }
-#if LANES_EARLY
   // nothing due anywhere in the wave (15 % of C3's wave-ticks, mostly drain tails): the tick
   // ends here -- phase A already counted its peeks, and B, the completion check and C/D
   // would change nothing
@@ -356,7 +346,6 @@ __device__ __forceinline__ bool tick(const Ctx& x, State<T>& s, bool act) {
     for (int v = 0; v < N; ++v) any |= pk[v];
     if (!__ballot(any != 0)) return true;
   }
-#endif
   // ---- B: receive, in-links in ascending sender rank ----------------------------------------
   // Straight-line and predicated: every register update happens on every lane (selects), only
   // the two snapshot-record stores sit in (divergent) branches -- register writes inside a
@@ -775,7 +764,7 @@ __device__ __forceinline__ void program(const ExecParams& p, const Op* __restric
         const bool act = s.alive && iter < until;
         if (!__ballot(act)) break;
         const bool idle = tick<T, SPILL>(x, s, act);
-        if (LANES_TAIL && idle && !anyw) {
+        if (idle && !anyw) {
           // no lane picked anything: if nothing is queued anywhere in the wave either, every
           // remaining tick of this op is empty for every lane (no peek, draw or delivery; the
           // drain tail after the last delivery, all of C3's idle wave-ticks) -- add them at once

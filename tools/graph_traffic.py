@@ -4,8 +4,8 @@ usage: python tools/graph_traffic.py <cfg> <nodes> <ticks> [drain]
 (env PMCG_DIR: the passes' directory, default gpurun_out/pmcg_<cfg>; OUT_DIR: default profiles/)
 A run is k_reset + the tick kernels (k_hostops, k_tally, k_pick, k_marker, k_scan, k_push);
 the post-run checks (k_finish, k_checks_*) are excluded.  Runs = k_reset dispatches.
-Bytes follow MI355X_MICROARCH.md's gfx950 correction as tools/make_profiles.py does:
-(2 * FETCH_SIZE + WRITE_SIZE) * 1024."""
+Bytes: raw (FETCH_SIZE + WRITE_SIZE) KB and fetch-doubled, per kernel, with the justified
+one (tools/traffic_model.py) as hbm_bytes_per_launch."""
 import collections
 import csv
 import glob
@@ -43,13 +43,23 @@ w, runs_w, wk = sums(os.path.join(base, "pass4", "**", "*counter_collection.csv"
 assert runs_f and runs_w, "no k_reset dispatches found"
 fetch_kb = f["FETCH_SIZE"] / runs_f
 write_kb = w["WRITE_SIZE"] / runs_w
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import traffic_model as tm  # noqa: E402
+per = {}
+for k in sorted(set(fk) | set(wk)):
+    r, co, j = tm.bytes_both(fk[k] / runs_f, wk[k] / runs_w, tm.streaming(k))
+    per[k] = {"raw": r, "corrected": co, "justified": j, "fetch_correction": tm.streaming(k), "reason": tm.reason(k)}
 out = {"config": cfg, "nodes": nodes, "steps": ticks, "drain": drain, "runs_profiled": runs_f,
        "fetch_kb_per_run": fetch_kb, "write_kb_per_run": write_kb,
-       "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024,
-       "per_kernel_bytes_per_run": {k: (2 * fk[k] / runs_f + wk[k] / runs_w) * 1024 for k in sorted(fk)},
+       "raw_bytes_per_launch": sum(v["raw"] for v in per.values()),
+       "corrected_bytes_per_launch": sum(v["corrected"] for v in per.values()),
+       "hbm_bytes_per_launch": sum(v["justified"] for v in per.values()),
+       "per_kernel": per,
        "per_kernel_fetch_kb_per_run": {k: fk[k] / runs_f for k in sorted(fk)},
        "per_kernel_write_kb_per_run": {k: wk[k] / runs_w for k in sorted(wk)},
-       "note": "one launch = one full run of the tick pipeline; (2*FETCH_SIZE + WRITE_SIZE) KB per gfx950 correction"}
+       "note": "one launch = one full run of the tick pipeline; raw = (FETCH_SIZE + WRITE_SIZE) KB, corrected = "
+               "(2 FETCH_SIZE + WRITE_SIZE) KB (the guide's gfx950 factor, for wide coalesced streaming reads only); "
+               "per kernel the justified figure is raw unless its reads are such streams (tools/traffic_model.py)"}
 out_dir = os.environ.get("OUT_DIR") or os.path.join(ROOT, "profiles")
 os.makedirs(out_dir, exist_ok=True)
 json.dump(out, open(os.path.join(out_dir, f"traffic_{cfg}.json"), "w"), indent=1)

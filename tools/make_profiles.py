@@ -5,8 +5,8 @@ usage: python tools/make_profiles.py <round> <cfg> [instances] [timed steps] [di
 writes profiles/<round>_<cfg>_kernel_stats.csv  (rocprofv3 --kernel-trace --stats)
        profiles/<round>_<cfg>_pmc.json          (per-dispatch PMC means, timed dispatches)
        profiles/traffic_<cfg>.json              (HBM bytes per launch for bench.py)
-HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KB; FETCH_SIZE
-reads 1/2 of a wide coalesced stream on gfx950, so bytes = (2 * FETCH + WRITE) * 1024.
+HBM bytes: FETCH_SIZE/WRITE_SIZE are KB; both raw and fetch-doubled figures are written
+(tools/traffic_model.py: the doubling is for wide coalesced streaming reads only).
 """
 import collections
 import csv
@@ -63,10 +63,14 @@ def main():
                            "max); SQ_* cycle counters are quad-cycles",
                    "counters": summary}, f, indent=1, sort_keys=True)
     if "FETCH_SIZE" in summary and "WRITE_SIZE" in summary:
-        hbm = (2 * summary["FETCH_SIZE"] + summary["WRITE_SIZE"]) * 1024
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import traffic_model as tm
+        raw, cor, just = tm.bytes_both(summary["FETCH_SIZE"], summary["WRITE_SIZE"], tm.streaming("cl_exec_kernel"))
         with open(os.path.join(out, f"traffic_{cfg}.json"), "w") as f:
             json.dump({"config": cfg, "instances": inst, "fifo_slots": 0,
-                       "hbm_bytes_per_launch": hbm, "fetch_kb": summary["FETCH_SIZE"],
+                       "hbm_bytes_per_launch": just, "raw_bytes_per_launch": raw,
+                       "corrected_bytes_per_launch": cor, "fetch_correction": False,
+                       "reason": tm.reason("cl_exec_kernel"), "fetch_kb": summary["FETCH_SIZE"],
                        "write_kb": summary["WRITE_SIZE"], "round": rnd}, f, indent=1)
     for row in csv.DictReader(open(stats)):
         if is_exec(row["Name"]):
