@@ -217,10 +217,11 @@ struct ColumnC {
 // read by the kernel at its start.
 constexpr int32_t kLanesMaxNodes = 16;
 constexpr int32_t kLanesMaxDegree = 4;
-// AUTO picks the instance-per-lane kernel only from this batch size up: one wave per 64
-// instances needs >= 4 waves per SIMD (1024 SIMDs) to hide its issue latency; smaller batches
-// run faster node-parallel (C2, 65,536 instances: 0.31 ms per step on lanes vs 0.153 ms)
-constexpr int64_t kLanesAutoMinInstances = 1 << 18;
+// AUTO picks the instance-per-lane kernel from this batch size up, for topologies with a
+// degree of 2 or more (measured, gpurun_out/r05p, ms per replay node-parallel / lanes: C3
+// 8nodes at 2^16 0.153 / 0.201, 2^17 0.289 / 0.232, 2^18 0.533 / 0.452, 2^19 1.055 / 0.925;
+// C2's ring (degree 1, the node-parallel kernel's cheapest shape) at 2^17 0.276 / 0.306)
+constexpr int64_t kLanesAutoMinInstances = 1 << 17;
 struct LanesTopo {
   int32_t ok;                       // the topology fits the kernel (set by the host)
   uint32_t node[kLanesMaxNodes];    // indeg (3..0) | outdeg (7..4) | out_off (15..8)

@@ -796,7 +796,8 @@ struct cl_sim {
     // degree <= 4) and the batch fills the chip with one instance per lane (AUTO); the
     // node-parallel kernel otherwise, or when run-time compilation failed
     const bool lanes = engine != CL_ENGINE_NODES && lanes_fit(p) &&
-                       (engine == CL_ENGINE_LANES || (int64_t)n_inst >= kLanesAutoMinInstances);
+                       (engine == CL_ENGINE_LANES ||
+                        ((int64_t)n_inst >= kLanesAutoMinInstances && std::max(max_out, max_in) >= 2));
     if (engine == CL_ENGINE_LANES && !lanes)
       return set_err(CL_E_LIMIT, "the instance-per-lane kernel needs <= %d nodes, degrees <= %d, <= 16 snapshots",
                      kLanesMaxNodes, kLanesMaxDegree);

@@ -1,6 +1,6 @@
 """A/B timing of the instance-per-lane kernel on a headline batch: per variant (a value of
 CLSNAP_LANES_DEFS, set by the caller), kernel ms per replay and the checksums against the
-node-parallel engine's.  usage: python tools/lanes_ab.py [c3|c2] [reruns] [lanes|nodes|auto]"""
+node-parallel engine's.  usage: python tools/lanes_ab.py [c3|c2] [reruns] [lanes|nodes|auto] [instances]"""
 import importlib, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 m = importlib.import_module("chandy-lamport-distributed-snapshot-algorithm_amd")
@@ -12,6 +12,8 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 eng = {"lanes": m.ChandyLamportSim.ENGINE_LANES, "nodes": m.ChandyLamportSim.ENGINE_NODES,
        "auto": m.ChandyLamportSim.ENGINE_AUTO}[sys.argv[3] if len(sys.argv) > 3 else "lanes"]
 top, ev, n = cfgs[name]
+if len(sys.argv) > 4:
+    n = int(sys.argv[4])
 s = m.ChandyLamportSim(n_instances=n)
 s.set_exec_engine(eng)
 s.read_topology_file(G + top)
@@ -25,5 +27,5 @@ for _ in range(reps):
     s.rerun()
 s.synchronize()
 tot, k = s.kernel_time()
-print(f"{name} engine={s.exec_engine()} variant={os.environ.get('CLSNAP_VARIANT', '')} defs={os.environ.get('CLSNAP_LANES_DEFS', '')!r} rerun_ms={tot / k:.4f} "
+print(f"{name} n={n} engine={s.exec_engine()} variant={os.environ.get('CLSNAP_VARIANT', '')} defs={os.environ.get('CLSNAP_LANES_DEFS', '')!r} rerun_ms={tot / k:.4f} "
       f"sums={s.checksums().tolist()}", flush=True)
