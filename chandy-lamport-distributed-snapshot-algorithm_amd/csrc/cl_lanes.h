@@ -248,7 +248,7 @@ __device__ __forceinline__ void push(const Ctx& x, uint32_t& hw, uint32_t ch, bo
     }
   }
   hw += ok ? 1u : 0u;
-  npush += ok ? 1u : 0u;
+  (void)npush;  // (pushes are derived at the epilogue: pops + packets still queued)
   nf = (on && !ok) ? (dly_ok ? (int32_t)ST_FIFO_OVERFLOW : (int32_t)ST_DELAY_EXHAUSTED) : nf;
 }
 
@@ -787,7 +787,7 @@ __device__ __forceinline__ void program(const ExecParams& p, const Op* __restric
   if (!valid) return;
   const uint32_t cap = 1u << capl;
   int32_t inflight = 0;
-  uint32_t ptok = 0, pmk = 0;
+  uint32_t ptok = 0, pmk = 0, queued = 0;
 #pragma unroll
   for (int v = 0; v < N; ++v) {
 #pragma unroll
@@ -796,6 +796,7 @@ __device__ __forceinline__ void program(const ExecParams& p, const Op* __restric
       if (k >= T::od(v)) continue;
       const uint32_t w = s.hw[v][k], cnt = w & 0x7fu, head = (w >> 7) & 0xffu;
       const uint32_t c = T::off(v) + k;
+      queued += cnt;
       for (uint32_t q = 0; q < cnt && q < cap; ++q) {
         const uint32_t e = fifo_rd(x, (c << capl) + ((head + q) & (cap - 1)));
         if (!(e & 0x8000u)) inflight += (int32_t)((e >> 8) & 0x7fu);
@@ -825,7 +826,10 @@ __device__ __forceinline__ void program(const ExecParams& p, const Op* __restric
   r[R_PEEK] = (int32_t)s.peek;
   r[R_POP_TOK] = (int32_t)ptok;
   r[R_POP_MK] = (int32_t)pmk;
-  r[R_PUSH] = (int32_t)s.push;
+  // Queue.Push count (queue.go:18-20) derived like the pops: every packet pushed since the
+  // program's start was either popped or is still queued (LDS ring or HBM spill ring)
+  const uint32_t pushes = ptok + pmk + queued;
+  r[R_PUSH] = (int32_t)pushes;
   r[R_INFLIGHT_TOK] = inflight;
 #pragma unroll
   for (int v = 0; v < N; ++v) p.fin_tok[inst * (uint32_t)N + v] = s.tok[v];
@@ -867,7 +871,7 @@ __device__ __forceinline__ void program(const ExecParams& p, const Op* __restric
     R[G_PEEK * st] = v == 0 ? s.peek : 0u;
     R[G_POP_TOK * st] = v == 0 ? ptok : 0u;  // (informational: a continuation derives them again)
     R[G_POP_MK * st] = v == 0 ? pmk : 0u;
-    R[G_PUSH * st] = v == 0 ? s.push : 0u;
+    R[G_PUSH * st] = v == 0 ? pushes : 0u;
   }
   uint32_t* Dn = S + (uint32_t)N * (lay.priv + G_NUM) * st;
   for (int32_t sid = 0; sid < lay.s_cap; ++sid) {
