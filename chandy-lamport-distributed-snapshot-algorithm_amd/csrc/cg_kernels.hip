@@ -247,16 +247,6 @@ __device__ inline void complete_nodes(const GParams& p, bool done, int32_t sid, 
 template <bool TRAIL>
 __device__ inline void block_exclusive_scan2_32(uint32_t& a, uint32_t& b, uint32_t& tot_a, uint32_t& tot_b,
                                                 uint32_t* sh);
-// (every caller's block totals fit 32 bits: one tick's triggers, sends, in-degree sums)
-__device__ inline void block_exclusive_scan2(long long& a, long long& b, long long& tot_a, long long& tot_b,
-                                             long long* sh /* [2 * 16] */) {
-  uint32_t a32 = (uint32_t)a, b32 = (uint32_t)b, ta, tb;
-  block_exclusive_scan2_32(a32, b32, ta, tb, reinterpret_cast<uint32_t*>(sh));
-  a = a32;
-  b = b32;
-  tot_a = ta;
-  tot_b = tb;
-}
 
 // Block tally of node rank v = blockIdx.x * kGThreads + threadIdx.x: `trig` draws
 // triggered by v's delivery this tick, and v's traffic send of step `step`.
@@ -291,14 +281,14 @@ __device__ inline void tally_sends(const GParams& p, int32_t bk, int32_t sendbit
 }
 
 __device__ inline void tally(const GParams& p, int32_t bk, int32_t trig, int32_t sendbit) {
-  __shared__ long long sh[2 * (kGThreads / 64)];
+  // (a block's totals fit 32 bits: its trigger draws are out-degrees, an int32 CSR span, and its
+  // sends one per node)
+  __shared__ uint32_t sh[2 * (kGThreads / 64)];
   const int v = bk * kGThreads + threadIdx.x;
-  long long a = trig, b = sendbit;
-  const long long a0 = a, b0 = b;
-  long long ta, tb;
-  block_exclusive_scan2(a, b, ta, tb, sh);
-  if (a0) p.ltrig[v] = (int32_t)a;
-  if (b0) p.lsend[v] = (int32_t)b;
+  uint32_t a = (uint32_t)trig, b = (uint32_t)sendbit, ta, tb;
+  block_exclusive_scan2_32(a, b, ta, tb, sh);
+  if (trig) p.ltrig[v] = (int32_t)a;
+  if (sendbit) p.lsend[v] = (int32_t)b;
   if (threadIdx.x == 0) {
     p.bsum[2 * bk] = ta;
     p.bsum[2 * bk + 1] = tb;
@@ -1029,7 +1019,7 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
   constexpr int kChunk = 2 * kGThreads;  // descriptors staged in LDS at a time (16 KB)
   __shared__ BigX sx[kChunk];
   __shared__ int32_t spre[kChunk + 1];
-  __shared__ long long ssh[2 * (kGThreads / 64)];
+  __shared__ uint32_t ssh[2 * (kGThreads / 64)];
   const int64_t gt = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
   for (int c0 = 0; c0 < nb; c0 += kChunk) {
     const int m = nb - c0 < kChunk ? nb - c0 : kChunk;
@@ -1044,8 +1034,9 @@ __global__ void __launch_bounds__(kGThreads) k_push(GParams p, int32_t targ, int
       sx[j0 + 1] = p.big[c0 + j0 + 1];
       len1 = sx[j0 + 1].hi - sx[j0 + 1].lo;
     }
-    long long a = len0 + len1, z = 0, tot, tz;
-    block_exclusive_scan2(a, z, tot, tz, ssh);
+    // (a chunk's in-degree sum is a span of the int32 in-CSR: 32 bits)
+    uint32_t a = (uint32_t)(len0 + len1), z = 0, tot, tz;
+    block_exclusive_scan2_32(a, z, tot, tz, ssh);
     spre[j0] = (int32_t)a;
     spre[j0 + 1] = (int32_t)(a + len0);
     if (threadIdx.x == 0) spre[kChunk] = (int32_t)tot;
@@ -1437,6 +1428,7 @@ int cg_launch_reset(const GParams& p, const int32_t* init_tok, void* stream) {
     const int64_t nsn = (int64_t)p.s_cap * p.n;
     const int64_t grid = nsn / kThreads + 1 < 65536 ? nsn / kThreads + 1 : 65536;
     hipLaunchKernelGGL(k_sn_reset, dim3((unsigned)grid), dim3(kThreads), 0, s, p.sn, nsn);
+    if ((e = hipGetLastError())) return e;
   }
   if ((e = hipMemsetAsync(p.done, 0, (size_t)p.s_cap * (1 + p.n_pblocks) * sizeof(int32_t), s))) return e;
   if ((e = hipMemsetAsync(p.sc, 0, sizeof(GScal), s))) return e;
