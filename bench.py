@@ -388,6 +388,11 @@ def main(argv=None):
                                   f"average kernel time, peak {world} x {HBM_PEAK_GBS:g} GB/s",
                          "valu": valu,
                          "binding_resource": (
+                             "instruction issue per wave: the instance-per-lane kernel runs 2 waves per SIMD "
+                             "(register-capped), so each wave's own issue rate (one VALU per 4 cycles) binds "
+                             "while the SIMD could take one per 2; neither the B_alg HBM fraction nor the VALU "
+                             "issue fraction is near 1 (DESIGN.md sections 5 and 9)"
+                             if engine == cl.ChandyLamportSim.ENGINE_LANES else
                              "instruction issue per wave-tick at ~5 resident waves per SIMD (LDS-capped): "
                              "neither the B_alg HBM fraction nor the VALU issue fraction is near 1; "
                              "fewer issued instructions (register pressure, compile-time LDS offsets) "

@@ -22,7 +22,10 @@ if prof is not None:
     c = {k: (v * scale if k != "SQ_WAVE_CYCLES" and k != "GRBM_GUI_ACTIVE" else v) for k, v in doc["counters"].items()}
     r = d["roofline"]
     kms = r["kernel_ms"]
-    r["traffic"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+    # raw bytes (the exec kernels' reads are not wide coalesced streams: tools/traffic_model.py)
+    r["traffic"] = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+    r["traffic_detail"] = {"raw": r["traffic"], "fetch_doubled": (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024,
+                           "write": c["WRITE_SIZE"] * 1024, "used": "raw", "source": os.path.relpath(p, ROOT)}
     rate = c["SQ_INSTS_VALU"] / (kms * 1e-3)
     r["valu"] = {"achieved": rate, "peak": bench.VALU_PEAK, "unit": "wave64 VALU instr/s",
                  "frac": rate / bench.VALU_PEAK, "insts_per_launch": c["SQ_INSTS_VALU"],
