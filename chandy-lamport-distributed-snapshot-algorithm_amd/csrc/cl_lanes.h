@@ -70,7 +70,8 @@ constexpr int rec_w(int D) { return D == 1 ? 2 : D <= 3 ? 4 : 8; }
 //   lane l at byte i * 128 + l * 2 (FW = E << CAPL >> 1 words of 256 bytes in all)
 //   then 32-bit words, word w of lane l at byte w * 256 + l * 4:
 //     FW            scratch word (stores that do not happen land here)
-//     FW + 1 ..     the delay row, 8 nibbles per word, then PAD zero words
+//     FW + 1 ..     the delay row, 8 nibbles per word (reads clamped to its last word: a
+//                   window past the end only feeds pushes past `draws`, which fail anyway)
 // A 16-bit FIFO entry: bits 7..0 receiveTime mod 256, bits 14..8 payload (token count or
 // snapshot id, < 128), bit 15 marker.  receiveTime is recovered from its low byte because an
 // entry is never more than draws + 4 ticks late when it is examined: while it is due but not
@@ -87,6 +88,7 @@ struct Ctx {
   uint32_t lrec;    // byte offset of this instance's node records in snapshot plane 0
   uint32_t plane8;  // bytes per snapshot plane / 256 (the stride is a multiple of 64)
   int32_t draws;    // delays per instance
+  uint32_t dlast;   // column word of the delay row's last word
 };
 
 __device__ __forceinline__ lds_u32* lds_at(uint32_t byte) { return (lds_u32*)(size_t)byte; }
@@ -107,8 +109,8 @@ struct Lds {
   static constexpr uint32_t CAPM7 = (CAP - 1u) << 7;  // a head word's ring-slot byte offset bits
   static constexpr uint32_t FW = ((uint32_t)T::E << T::CAPL) / 2;
   static constexpr uint32_t DUMMY = FW, DB = FW + 1;
-  // zero words after the delay row: the tick's delay window may reach past its end
-  static constexpr uint32_t PAD = (7 + T::E + 7) / 8 + 1;
+  // words of a tick's delay window (reads past the row's end are clamped to its last word)
+  static constexpr uint32_t WIN = (7 + T::E + 7) / 8 + 1;
 };
 // receiveTime <= time for a 16-bit entry (see the layout note): 1 or 0
 __device__ __forceinline__ uint32_t due16(uint32_t e, int32_t time) {
@@ -127,7 +129,7 @@ __device__ __forceinline__ uint32_t e32_to_16(uint32_t e) {
 template <class T>
 __device__ __forceinline__ uint32_t delays8(const Ctx& x, int32_t k) {
   const uint32_t w = Lds<T>::DB + ((uint32_t)min(k, x.draws) >> 3);
-  const uint32_t lo = col_rd(x, w), hi = col_rd(x, w + 1);
+  const uint32_t lo = col_rd(x, min(w, x.dlast)), hi = col_rd(x, min(w + 1, x.dlast));
   return __builtin_amdgcn_alignbit(hi, lo, ((uint32_t)k & 7u) * 4u);
 }
 
@@ -441,12 +443,12 @@ __device__ __forceinline__ bool tick(const Ctx& x, State<T>& s, bool act) {
     }
     // the tick's delays in one LDS round trip: draws [draw, draw + acc) lie in the WN words
     // from draw / 8 (acc <= E: each channel carries at most one broadcast push per tick)
-    constexpr int WN = (int)Lds<T>::PAD;
+    constexpr int WN = (int)Lds<T>::WIN;
     uint32_t dw[WN];
     {
       const uint32_t w0 = Lds<T>::DB + ((uint32_t)min(s.draw, x.draws) >> 3);
 #pragma unroll
-      for (int q = 0; q < WN; ++q) dw[q] = col_rd(x, w0 + q);
+      for (int q = 0; q < WN; ++q) dw[q] = col_rd(x, min(w0 + q, x.dlast));
     }
 #pragma unroll
     for (int v = 0; v < N; ++v) {
@@ -639,7 +641,8 @@ __device__ __forceinline__ void program(const ExecParams& p, const Op* __restric
               st,
               4u * inst * (uint32_t)N * (uint32_t)RW,
               (4u * st * (uint32_t)N * (uint32_t)RW) >> 8,
-              (int32_t)(p.draws < 0x7fffffffLL ? p.draws : 0x7fffffffLL)};
+              (int32_t)(p.draws < 0x7fffffffLL ? p.draws : 0x7fffffffLL),
+              Lds<T>::DB + nd - 1};
 
   // The instance's delay row, packed to nibbles (delays are < maxDelay = 5), in the column.
   if (valid) {
@@ -653,8 +656,6 @@ __device__ __forceinline__ void program(const ExecParams& p, const Op* __restric
       col_wr(x, Lds<T>::DB + 2 * q + 1, nib(b.z) | (nib(b.w) << 16));
     }
   }
-#pragma unroll
-  for (uint32_t q = 0; q < Lds<T>::PAD; ++q) col_wr(x, Lds<T>::DB + nd + q, 0u);
 
   State<T> s;
   s.flag = 0;
