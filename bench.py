@@ -274,6 +274,9 @@ def main(argv=None):
     collect = collect_all(sim, args) if not args.no_collect else None
     engine = sim.exec_engine()
     spilled, split = sim.replay_split()
+    # (cl_jit.cpp launch_lanes: the spilling half runs on the lanes spill kernel when it fills a
+    # wave per SIMD, node-parallel otherwise)
+    spill_on_lanes = spilled >= 64 * 4 * torch.cuda.get_device_properties(device).multi_processor_count
     replay = {"slot_map": sim.mapped_replays(), "spill_free": sim.spill_free_replays(),
               "spilled_instances": spilled, "split_slot": split}
     fresh = fresh_run(cl, per_rank, device, seed_base + total, top, events, args) if not args.no_fresh else None
@@ -381,17 +384,18 @@ def main(argv=None):
                          "frac": hbm_frac,
                          "traffic": traffic, "traffic_detail": traffic_detail,
                          "kernel": ("clsnap_lanes_nospill (instance per lane, hipRTC-specialized to the "
-                                    "topology)" + (" + cl_exec_kernel on the spilling instances" if split else "")
+                                    "topology)" + ((" + clsnap_lanes_spill" if spill_on_lanes else " + cl_exec_kernel")
+                                                   + " on the spilling instances" if split else "")
                                     if engine == cl.ChandyLamportSim.ENGINE_LANES else "cl_exec_kernel"),
                          "kernel_ms": avg_kernel_ms, "alg_bytes_per_launch": alg,
                          "scope": f"whole node: {world} GPU(s), bytes summed over ranks, slowest rank's "
                                   f"average kernel time, peak {world} x {HBM_PEAK_GBS:g} GB/s",
                          "valu": valu,
                          "binding_resource": (
-                             "instruction issue per wave: the instance-per-lane kernel runs 2 waves per SIMD "
-                             "(register-capped), so each wave's own issue rate (one VALU per 4 cycles) binds "
-                             "while the SIMD could take one per 2; neither the B_alg HBM fraction nor the VALU "
-                             "issue fraction is near 1 (DESIGN.md sections 5 and 9)"
+                             "instruction issue per wave: the instance-per-lane kernel runs 3 waves per SIMD "
+                             "(168 VGPRs, 13 KB of LDS per wave), each wave bound by its own dependent chains "
+                             "(one VALU per 4 cycles at most, the SIMD could take one per 2); neither the B_alg "
+                             "HBM fraction nor the VALU issue fraction is near 1 (DESIGN.md sections 5 and 9)"
                              if engine == cl.ChandyLamportSim.ENGINE_LANES else
                              "instruction issue per wave-tick at ~5 resident waves per SIMD (LDS-capped): "
                              "neither the B_alg HBM fraction nor the VALU issue fraction is near 1; "

@@ -266,8 +266,8 @@ struct cl_sim {
   // Fold finished launch timings into the accumulator so the event pool stays bounded.
   int fold_events() {
     HIP_TRY(hipStreamSynchronize(stream));
-    // (a pipelined replay's start event is recorded on stream2, which `stream` may not have
-    // joined yet: cl_rerun folds every 256 launches without a join)
+    // (a pipelined replay's spill-capable stop event is recorded on stream2, which `stream` may
+    // not have joined yet: cl_rerun folds every 256 launches without a join)
     if (stream2) HIP_TRY(hipStreamSynchronize(stream2));
     for (size_t i = 0; i < ev_used; ++i) {
       float f = 0.f;
@@ -786,12 +786,15 @@ struct cl_sim {
     // the dispatch records both events (the kernel's own start/end timestamps): two
     // hipEventRecord packets around it cost 0.7 us more per launch (C2 0.1816 -> 0.1809 ms per
     // step) and bracketed ~1 us of packet processing into the kernel time
-    // split replays back to back fork stream2 from `stream` but do not join it (r03 A/B: joining
-    // every replay, or neither forking nor joining, measured slower)
+    // split replays back to back do not join stream2 (r03 A/B: joining every replay measured slower)
     const bool pipe = planned && p.split_slot > 0 && p.split_slot < n_inst && stream2 && !save_state;
     if (!pipe && (rc = join_stream2())) return rc;
-    const ExecLaunch el{stream, pr.start, pr.stop, stream2, ev_fork, ev_join, 1, pipe ? 0 : 1, pr.stop2,
-                        &pr.stop2_used};
+    // (a replay's stream2 half waits for `stream` only when `stream` got other work since the
+    // last fork: consecutive replays touch disjoint instances on the two streams.  C3 per replay,
+    // forking every replay / only then: 2^17 0.2391-0.2394 / 0.2370-0.2371 ms, 2^20
+    // 1.6146-1.6151 / 1.6104-1.6113 ms, gpurun_out/r05z)
+    const ExecLaunch el{stream, pr.start, pr.stop, stream2, ev_fork, ev_join, (!pipe || s_dirty) ? 1 : 0,
+                        pipe ? 0 : 1, pr.stop2, &pr.stop2_used};
     // the instance-per-lane kernel, compiled for this topology, wherever it fits (N <= 16, every
     // degree <= 4) and the batch fills the chip with one instance per lane (AUTO); the
     // node-parallel kernel otherwise, or when run-time compilation failed

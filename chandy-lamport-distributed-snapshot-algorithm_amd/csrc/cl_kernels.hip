@@ -1242,8 +1242,8 @@ int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, con
 // A replay split by the plan of its first run (cl_host.cpp build_plan): the slot map puts the
 // instances whose queues outgrew the LDS rings last; slots [0, split) run on the spill-free
 // kernel (6 waves per SIMD for D = 3, 4), slots [split, n) on the spill-capable one,
-// concurrently on a second stream (fork / join events).  The spill-capable dispatch records the
-// start event; the main dispatch the stop event, or a record after the join.
+// concurrently on a second stream (fork / join events).  The main dispatch records the start
+// event and the stop event (a record after the join when joined); the spill-capable one its own stop.
 template <int D, int CAP>
 int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched,
                       const ExecLaunch& L) {
@@ -1256,19 +1256,19 @@ int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, 
   a.n_inst = p.split_slot;
   b.slot_base = (uint32_t)p.split_slot;
   ExecLaunch la = L;
-  // unjoined, the main dispatch records the stop event itself: a separate record packet
-  // between back-to-back replays held the next dispatch ~8 us (gpurun_out/r05t)
+  // the main dispatch records the start event and, unjoined, the stop event itself (a separate
+  // record packet between back-to-back replays held the next dispatch ~8 us, gpurun_out/r05t)
   if (L.join) la.ev_stop = nullptr;
   // the spill-capable dispatch records a stop event of its own (ev_stop2): unjoined, it may
   // end after the main stream's stop, and the launch time is the later of the two
   ExecLaunch lb = L;
+  lb.ev_start = nullptr;
   lb.ev_stop = L.ev_stop2;
   int e;
   // the spilling instances are the longest: their kernel is dispatched first so its
   // workgroups are resident from the start instead of queueing behind the main grid (the
-  // tail of a small per-GPU batch); it records the start event
+  // tail of a small per-GPU batch)
   if ((e = launch_exec_ds<D, true, false, CAP, true, true>(b, topo, ops, sched, lb, s2, true))) return e;
-  la.ev_start = nullptr;
   if ((e = launch_exec_ds<D, true, false, CAP, false, true>(a, topo, ops, sched, la))) return e;
   if (L.stop2_used && L.ev_stop2) *L.stop2_used = 1;
   if (!L.join) return 0;  // replays back to back: the main stream does not wait for stream2 (cl_host.cpp)
