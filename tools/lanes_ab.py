@@ -1,5 +1,5 @@
-"""A/B timing of the instance-per-lane kernel on a headline batch: per variant (a value of
-CLSNAP_LANES_DEFS, set by the caller), kernel ms per replay and the checksums against the
+"""A/B timing of the instance-per-lane kernel on a headline batch: per variant (a cl_lanes.h
+copy named by CLSNAP_LANES_HEADER, or a build), kernel ms per replay and the checksums against the
 node-parallel engine's.  usage: python tools/lanes_ab.py [c3|c2] [reruns] [lanes|nodes|auto] [instances]"""
 import importlib, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -29,5 +29,5 @@ for _ in range(reps):
     s.rerun()
 s.synchronize()
 tot, k = s.kernel_time()
-print(f"{name} n={n} engine={s.exec_engine()} variant={os.environ.get('CLSNAP_VARIANT', '')} defs={os.environ.get('CLSNAP_LANES_DEFS', '')!r} rerun_ms={tot / k:.4f} fresh_ms={fresh_ms:.4f} "
+print(f"{name} n={n} engine={s.exec_engine()} variant={os.environ.get('CLSNAP_VARIANT', '')} rerun_ms={tot / k:.4f} fresh_ms={fresh_ms:.4f} "
       f"sums={s.checksums().tolist()}", flush=True)
