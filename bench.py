@@ -81,7 +81,9 @@ PARITY_KEYS = ("instances", "ok", "fatal", "other", "delivered", "snapshot_hash"
 # Default (steps, warmup) per config: enough untimed launches for the GPU's clocks to settle
 # (C2's 0.18 ms launches measured 0.185 ms per kernel over 3 warmup + 30 timed steps and
 # 0.176 ms over 300 timed steps) and a timed region of >= 50 ms.
-STEP_DEFAULTS = {"c2": (300, 100), "c3": (20, 10)}
+# (timed steps, warmup): enough timed replays that the two stream synchronisations of the timed
+# region stay under 1 % of it (C3: 200 x 1.64 ms)
+STEP_DEFAULTS = {"c2": (300, 100), "c3": (200, 20)}
 
 
 def parse_args(argv=None):

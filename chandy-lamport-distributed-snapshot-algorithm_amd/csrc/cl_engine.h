@@ -311,11 +311,12 @@ struct ExecLaunch {
   // stream (new work there since the last fork), join = the engine stream waits for stream2
   // before the stop event (else the join is deferred to the next call that is not a rerun)
   int32_t fork, join;
-  // split replays: the spill-capable dispatch records this stop event of its own (it may end
-  // after the main stream's stop event when the replays are not joined); *stop2_used is set
-  // to 1 when it was recorded, and the launch time is the later of the two stops
+  // split replays: the spill-capable dispatch records start and stop events of its own (its
+  // half may end after the main stream's stop event when the replays are not joined);
+  // *stop2_used is set to 1 when they were recorded, and the launch time is the longer half
   void* ev_stop2;
   int32_t* stop2_used;
+  void* ev_start2;
 };
 int launch_exec(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched, const ExecLaunch& L);
 // The instance-per-lane kernel (cl_lanes.h, compiled per topology by cl_jit.cpp): lanes_fit

@@ -241,10 +241,11 @@ struct cl_sim {
   bool dev_ready = false;
   hipStream_t stream = nullptr;
   bool timed = false;
-  // per-launch timing events: start, stop, and the split replay's spill-capable stop (the
-  // launch time is from start to the later stop)
+  // per-launch timing events: start, stop, and the split replay's spill-capable start / stop
+  // (the launch time is the longer of the two concurrent halves: consecutive replays are not
+  // joined, so a half's own events, not the other stream's, bound it)
   struct LaunchEvents {
-    hipEvent_t start = nullptr, stop = nullptr, stop2 = nullptr;
+    hipEvent_t start = nullptr, stop = nullptr, start2 = nullptr, stop2 = nullptr;
     int32_t stop2_used = 0;
   };
   std::vector<LaunchEvents> ev_pool;
@@ -257,7 +258,7 @@ struct cl_sim {
     HIP_TRY(hipEventElapsedTime(ms, e.start, e.stop));
     if (e.stop2_used) {
       float f2 = 0.f;
-      HIP_TRY(hipEventElapsedTime(&f2, e.start, e.stop2));
+      HIP_TRY(hipEventElapsedTime(&f2, e.start2, e.stop2));
       *ms = std::max(*ms, f2);
     }
     return CL_OK;
@@ -379,6 +380,7 @@ struct cl_sim {
         (void)hipEventDestroy(e.start);
         (void)hipEventDestroy(e.stop);
         (void)hipEventDestroy(e.stop2);
+        (void)hipEventDestroy(e.start2);
       }
       if (stream2) (void)hipStreamDestroy(stream2);
       if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -778,6 +780,7 @@ struct cl_sim {
       HIP_TRY(hipEventCreateWithFlags(&le.start, hipEventDisableSystemFence));
       HIP_TRY(hipEventCreateWithFlags(&le.stop, hipEventDisableSystemFence));
       HIP_TRY(hipEventCreateWithFlags(&le.stop2, hipEventDisableSystemFence));
+      HIP_TRY(hipEventCreateWithFlags(&le.start2, hipEventDisableSystemFence));
       ev_pool.push_back(le);
     }
     ev_last = ev_used;
@@ -794,7 +797,7 @@ struct cl_sim {
     // forking every replay / only then: 2^17 0.2391-0.2394 / 0.2370-0.2371 ms, 2^20
     // 1.6146-1.6151 / 1.6104-1.6113 ms, gpurun_out/r05z)
     const ExecLaunch el{stream, pr.start, pr.stop, stream2, ev_fork, ev_join, (!pipe || s_dirty) ? 1 : 0,
-                        pipe ? 0 : 1, pr.stop2, &pr.stop2_used};
+                        pipe ? 0 : 1, pr.stop2, &pr.stop2_used, pr.start2};
     // the instance-per-lane kernel, compiled for this topology, wherever it fits (N <= 16, every
     // degree <= 4) and the batch fills the chip with one instance per lane (AUTO); the
     // node-parallel kernel otherwise, or when run-time compilation failed

@@ -1243,7 +1243,7 @@ int launch_exec_ds(const ExecParams& p, const uint32_t* topo, const Op* ops, con
 // instances whose queues outgrew the LDS rings last; slots [0, split) run on the spill-free
 // kernel (6 waves per SIMD for D = 3, 4), slots [split, n) on the spill-capable one,
 // concurrently on a second stream (fork / join events).  The main dispatch records the start
-// event and the stop event (a record after the join when joined); the spill-capable one its own stop.
+// event and the stop event (a record after the join when joined); the spill-capable one its own pair.
 template <int D, int CAP>
 int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, const uint8_t* sched,
                       const ExecLaunch& L) {
@@ -1259,10 +1259,10 @@ int launch_exec_split(const ExecParams& p, const uint32_t* topo, const Op* ops, 
   // the main dispatch records the start event and, unjoined, the stop event itself (a separate
   // record packet between back-to-back replays held the next dispatch ~8 us, gpurun_out/r05t)
   if (L.join) la.ev_stop = nullptr;
-  // the spill-capable dispatch records a stop event of its own (ev_stop2): unjoined, it may
-  // end after the main stream's stop, and the launch time is the later of the two
+  // the spill-capable dispatch records start and stop events of its own (ev_start2 / ev_stop2):
+  // unjoined, it may end after the main stream's stop, and the launch time is the longer half
   ExecLaunch lb = L;
-  lb.ev_start = nullptr;
+  lb.ev_start = L.ev_start2;
   lb.ev_stop = L.ev_stop2;
   int e;
   // the spilling instances are the longest: their kernel is dispatched first so its
