@@ -22,9 +22,10 @@ def _lanes_engine():
 
 
 def test_lanes_equals_nodes_headline_with_spills():
-    """2^20 instances of BASELINE config 3 with 2 LDS FIFO slots (a split replay: the spilling
-    instances on the node-parallel spill kernel, the rest on the lanes kernel) and with the
-    default layout: every output plane equal between the two engines."""
+    """2^20 instances of BASELINE config 3 with 2 LDS FIFO slots and with the default layout
+    (split replays: the spilling instances -- over 65,536 of them, a wave per SIMD -- on the lanes
+    spill kernel, the rest on the spill-free lanes kernel): every output plane equal between the
+    two engines."""
     top, events, n = "8nodes.top", "8nodes-concurrent-snapshots.events", 1 << 20
     for slots in (None, 2):
         out = {}
@@ -56,3 +57,31 @@ def test_lanes_refuses_what_it_cannot_run():
     sim2.read_events_text("snapshot H\n")
     sim2.flush()
     assert sim2.exec_engine() == cl.ChandyLamportSim.ENGINE_NODES
+
+
+@pytest.mark.parametrize("n", [1 << 17, 1 << 20])
+def test_back_to_back_split_replays(n):
+    """Split replays back to back do not fork the second stream from the main one (they touch
+    disjoint instances): 2^17 instances put the spilling half on the node-parallel kernel, 2^20
+    on the lanes spill kernel.  Ten replays in a row leave the same outputs as one, and a launch's
+    kernel time (the longer half, each timed by its own events) stays within the wall time of a
+    replay -- a half timed from the other stream's events would count the queueing."""
+    import time
+    sim = engine_run("8nodes.top", "8nodes-concurrent-snapshots.events", n)
+    sim.rerun()
+    sim.synchronize()
+    spilled, split = sim.replay_split()
+    assert 0 < split < n and 0 < spilled <= n - split
+    one = (sim.checksums(), sim.status(), sim.counters(only_ok=False))
+    sim.kernel_time()
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sim.rerun()
+    sim.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3 / reps
+    k_total, k_n = sim.kernel_time()
+    assert k_n == reps
+    assert 0.5 * wall_ms < k_total / k_n < 1.2 * wall_ms
+    many = (sim.checksums(), sim.status(), sim.counters(only_ok=False))
+    assert np.array_equal(one[0], many[0]) and np.array_equal(one[1], many[1]) and one[2] == many[2]
