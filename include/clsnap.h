@@ -141,10 +141,11 @@ int cl_flush(cl_sim* sim);
  * half (they touch disjoint instances); every other call waits for it first. */
 int cl_rerun(cl_sim* sim);
 int cl_synchronize(cl_sim* sim);
-/* Device time of the most recent cl_flush/cl_rerun kernel, from HIP events on the
- * stream the kernel runs on. */
+/* Device time of the most recent cl_flush/cl_rerun kernel, from HIP events recorded by the
+ * kernel dispatches themselves; a split replay's time is the longer of its two concurrent
+ * halves, each timed by its own dispatch's events. */
 int cl_last_kernel_ms(cl_sim* sim, double* ms);
-/* Sum of exec-kernel device times (HIP events around every launch) since the previous
+/* Sum of exec-kernel device times (as cl_last_kernel_ms, every launch) since the previous
  * call, and the number of launches; resets the accumulator. */
 int cl_kernel_time(cl_sim* sim, double* total_ms, int64_t* launches);
 /* 1 in *on when the next cl_rerun runs wholly on the spill-free kernel: the layout has no HBM
