@@ -1446,7 +1446,7 @@ int cl_graph_get_counters(cl_graph* g, int64_t* out) {
   out[CL_CNT_PEEK] = (int64_t)cnt[GC_PEEK];
   out[CL_CNT_POP_TOKEN] = (int64_t)cnt[GC_POP_TOK];
   out[CL_CNT_POP_MARKER] = (int64_t)cnt[GC_POP_MK];
-  out[CL_CNT_RECORDED] = (int64_t)(cnt[GC_RECORDED] + open);
+  out[CL_CNT_RECORDED] = (int64_t)open;  // (k_finish: every created local snapshot's recorded copies)
   out[CL_CNT_COMPLETED] = (int64_t)cnt[GC_COMPLETED];
   out[CL_CNT_INSTANCES] = 1;
   out[CL_CNT_TICKS] = sc.status ? sc.time : g->time;

@@ -558,7 +558,7 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
     tally_sends(p, bk, sendbit);
     return;
   }
-  unsigned long long c[2] = {0, 0};  // recorded, completed
+  unsigned long long c[1] = {0};  // completed (the recorded copies are summed by k_finish)
   bool done = false;
   int32_t sid = 0, vdone = 0;
   int bslot = -1, cslot = -1;
@@ -599,9 +599,10 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
       // later marker: stop recording the channel (node.go:158-160)
       if ((key >> 32) != (uint64_t)t) {  // created in an earlier tick: cursors exist
         const uint32_t e = p.tokcnt[k];
-        uint32_t* r = (uint32_t*)&p.rec[(size_t)sid * p.e + k];
-        c[0] += e - r[0];
-        r[1] = e;
+        // (the end cursor only: k_finish sums end - begin when counters are read, so the close
+        // does not wait for the begin cursor; C5 3,840-3,870 -> 3,759-3,770 ms per run with the
+        // read dropped, gpurun_out/r05am)
+        reinterpret_cast<uint32_t*>(&p.rec[(size_t)sid * p.e + k])[1] = e;
       }  // else created this tick by a lower-ranked sender: its expansion closes it
       done = atomicAdd(&rn->cnt, -1) - 1 == kBig;
     }
@@ -610,9 +611,9 @@ __global__ void __launch_bounds__(kGThreads) k_marker(GParams p, int32_t targ) {
     const MDel m = list[threadIdx.x];
     gtrace(p, t, kTrTick, (uint32_t)m.s0, kTrSubEnd, TK_END, vdone, -1, sid);
   }
-  complete_nodes(p, done, sid, vdone, t, c[1]);
-  const int idx[2] = {GC_RECORDED, GC_COMPLETED};
-  block_count<2>(p, idx, c);  // (has a barrier: s_trig and s_nb are final below)
+  complete_nodes(p, done, sid, vdone, t, c[0]);
+  const int idx[1] = {GC_COMPLETED};
+  block_count<1>(p, idx, c);  // (has a barrier: s_trig and s_nb are final below)
   // one block scan for both: creations numbered in thread order (b), in-link pairs by the
   // prefix of in-degrees (a); and the tally (triggers c, traffic sends d)
   const bool cre = cslot >= 0;
@@ -1343,7 +1344,9 @@ __global__ void __launch_bounds__(kGThreads) k_part_rdraw(GParams p, const long 
 // ---------------------------------------------------------------------------
 // results
 // ---------------------------------------------------------------------------
-// Recorded copies of channels still recording at the end (HandleToken appended them).
+// Recorded copies (HandleToken appended them, node.go:179-183) of every created local snapshot:
+// end - begin of each closed channel, and the delivered count - begin of a channel still
+// recording.
 __global__ void k_finish(GParams p, int32_t n_sids, unsigned long long* out) {
   const size_t span = (size_t)(p.part_hi - p.part_lo);  // owned nodes
   const size_t total = (size_t)n_sids * span;
@@ -1351,12 +1354,12 @@ __global__ void k_finish(GParams p, int32_t n_sids, unsigned long long* out) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int32_t sid = (int32_t)(i / span), v = p.part_lo + (int32_t)(i % span);
     const size_t sv = (size_t)sid * p.n + v;
-    const SNode r0 = p.sn[sv];
-    if (r0.W == ~0ull || r0.cnt == kBig) continue;
+    if (p.sn[sv].W == ~0ull) continue;
     const uint64_t* r = p.rec + (size_t)sid * p.e;
     for (int32_t k = p.in_off[v]; k < p.in_off[v + 1]; ++k) {
       const uint64_t x = r[k];
-      if ((uint32_t)(x >> 32) == kOpen) rec += p.tokcnt[k] - (uint32_t)x;
+      const uint32_t b = (uint32_t)x, e = (uint32_t)(x >> 32);
+      rec += (e == kOpen ? p.tokcnt[k] : e) - b;
     }
   }
   wave_count(out, rec);
