@@ -278,7 +278,7 @@ def main(argv=None):
     spilled, split = sim.replay_split()
     # (cl_jit.cpp launch_lanes: the spilling half runs on the lanes spill kernel when it fills a
     # wave per SIMD, node-parallel otherwise)
-    spill_on_lanes = spilled >= 64 * 4 * torch.cuda.get_device_properties(device).multi_processor_count
+    spill_on_lanes = per_rank - split >= 64 * 4 * torch.cuda.get_device_properties(device).multi_processor_count
     replay = {"slot_map": sim.mapped_replays(), "spill_free": sim.spill_free_replays(),
               "spilled_instances": spilled, "split_slot": split}
     fresh = fresh_run(cl, per_rank, device, seed_base + total, top, events, args) if not args.no_fresh else None
